@@ -1,0 +1,107 @@
+"""ctypes binding of libfmx.so (the HIP/gfx950 kernels behind the drop-in API).
+
+There is no CPU fallback: if the shared library or a GPU is missing, every compute
+entry point raises :class:`FmxError`.  ``torch`` is imported first so that the HIP
+runtime torch ships with (``libamdhip64.so.7``) is the one libfmx binds to -- device
+pointers and streams are then shared between torch and libfmx.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before libfmx: one HIP runtime per process)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FMX_LIB", os.path.join(_HERE, "libfmx.so"))
+
+c_i32, c_i64, c_dbl, c_vp, c_cp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p, ctypes.c_char_p
+
+# name -> argtypes (restype is c_int32 = fmx_status unless listed in _RESTYPES)
+SIGNATURES = {
+    "fmx_last_error": [],
+    "fmx_abi_version": [],
+    "fmx_device_info": [c_cp, c_i64],
+    "fmx_ts_op": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
+    "fmx_ts_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
+    "fmx_ts_regression": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp],
+    "fmx_cs_moment": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
+    "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
+    "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
+    "fmx_cs_filter_center": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
+    "fmx_group_op": [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp],
+    "fmx_cs_regression": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
+    "fmx_elementwise": [c_i32, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_vp],
+    "fmx_bucket": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    "fmx_ic_daily": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
+    "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
+    "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
+    "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
+}
+_RESTYPES = {"fmx_last_error": c_cp}
+
+# constants mirrored from include/fmx.h
+TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)
+CS = dict(zscore=0, mean=1, market_neutralize=2)
+RANK = dict(average=0, min=1, max=2, first=3, dense=4)
+GROUP = dict(mean=0, neutralize=1, normalize=2, rank=3)
+EW = dict(sign=0, power=1, log=2, abs=3, clip=4, where=5)
+CSREG = dict(resid=0, beta=1, alpha=2, fitted=3, r2=4)
+
+
+class FmxError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = None):
+    """Load libfmx.so (no GPU needed) and bind every exported entry point."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise FmxError(f"libfmx.so not found at {p}; build it with __graft_entry__.build() "
+                           f"(make -C factormodeling_amd/csrc)")
+        lib = ctypes.CDLL(p)
+        for name, args in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, c_i32)
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise FmxError("factormodeling_amd needs an MI355X (HIP device); none is visible. "
+                       "There is no CPU fallback by design.")
+
+
+def call(name: str, *args):
+    """Invoke an fmx_* entry point and raise FmxError on a non-zero status."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != 0:
+        msg = lib.fmx_last_error()
+        raise FmxError(f"{name} failed (status {st}): {msg.decode() if msg else ''}")
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,584 @@
+// Cross-sectional (per-date) kernels: one 256-thread workgroup per (factor, date) row of
+// the [F][D][ld] panel.  The row (A contiguous fp64, asset-fastest) is staged in LDS
+// once and reduced/sorted there.
+//
+// Reference: operations.py:54-86 (cs_rank, cs_winsor, cs_filter_center, cs_zscore,
+// cs_bool, cs_mean), :88-101 (elementwise), :104-168 (bucket, group ops), :171-182
+// (market_neutralize), :248-304 (cs_regression).
+#include "rowkit.hpp"
+
+namespace fmx {
+
+constexpr int CS_NT = 256;
+
+// Stage the present values of row (f, d) into LDS v[0..n) in asset order and return n.
+// Dense rows (present == nullptr) map v[i] = x[i].  pos (optional, u16) records the asset
+// of each staged element for ragged rows.
+__device__ int stage_row(const double* __restrict__ x, const uint8_t* __restrict__ prow, int64_t A,
+                         double* v, uint16_t* pos, int* iscr) {
+  if (!prow) {
+    for (int64_t i = threadIdx.x; i < A; i += CS_NT) {
+      v[i] = x[i];
+      if (pos) pos[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    return (int)A;
+  }
+  const int64_t C = (A + CS_NT - 1) / CS_NT;
+  const int64_t a0 = threadIdx.x * C, a1 = min<int64_t>(A, a0 + C);
+  int cnt = 0;
+  for (int64_t a = a0; a < a1; ++a) cnt += prow[a] != 0;
+  int tot;
+  int base = block_exscan<CS_NT>(cnt, iscr, &tot);
+  for (int64_t a = a0; a < a1; ++a) {
+    if (prow[a]) {
+      v[base] = x[a];
+      if (pos) pos[base] = (uint16_t)a;
+      ++base;
+    }
+  }
+  __syncthreads();
+  return tot;
+}
+
+// ------------------------------------------------------------------------------------
+// cs_zscore / cs_mean / market_neutralize (nanops.nanmean / nanvar(ddof=0), pairwise)
+template <int OP>
+__global__ void __launch_bounds__(CS_NT)
+k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+            const uint8_t* __restrict__ present, PwTable pw) {
+  extern __shared__ double lds[];
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d) * ld;
+  double* y = Y + (f * D + d) * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  double* v = lds;                                   // [A]
+  uint16_t* pos = present ? (uint16_t*)(v + A) : nullptr;
+  double* nodes = (double*)((char*)(v + A) + (present ? ((A * 2 + 15) & ~15) : 0));  // [2A/64+8]
+  int* iscr = (int*)(nodes + (2 * (A / 64) + 8));
+  double* dscr = (double*)(iscr + 16);
+  const int n = stage_row(x, prow, A, v, pos, iscr);
+  if (n == 0) return;
+  const int32_t* sch = pw.get(n);
+  int c = 0;
+  for (int i = threadIdx.x; i < n; i += CS_NT) c += (v[i] == v[i]);
+  int cnt;
+  block_exscan<CS_NT>(c, iscr, &cnt);
+  double s1 = block_pw_sum<CS_NT>([&](int i) { double t = v[i]; return t == t ? t : 0.0; }, sch, nodes);
+  double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+  double sd = 0.0;
+  if (OP != FMX_CS_MEAN) {
+    double s2 = block_pw_sum<CS_NT>([&](int i) {
+      double t = v[i];
+      double z = t == t ? t : 0.0;
+      double q = (mean - z) * (mean - z);
+      return t == t ? q : 0.0;
+    }, sch, nodes);
+    double var = cnt > 0 ? s2 / (double)cnt : qnan();
+    sd = sqrt(var);
+  }
+  (void)dscr;
+  const bool guard = (OP == FMX_CS_MARKET_NEUTRALIZE) && (sd == 0.0 || sd != sd);
+  for (int i = threadIdx.x; i < n; i += CS_NT) {
+    double t = v[i];
+    double o;
+    if (OP == FMX_CS_MEAN) o = mean;
+    else if (guard) o = 0.0;
+    else o = (t - mean) / sd;
+    int64_t a = prow ? pos[i] : i;
+    y[a] = o;
+  }
+  if (prow) {
+    for (int64_t a = threadIdx.x; a < A; a += CS_NT)
+      if (!prow[a]) y[a] = qnan();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// cs_rank: pandas Series.rank(method) over non-NaN, (r-1)/(len-1) with len = #rows of the
+// date (NaN included), a single-row date -> 0.5.
+__global__ void __launch_bounds__(CS_NT)
+k_cs_rank(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+          int P, int method, const uint8_t* __restrict__ present) {
+  extern __shared__ uint64_t keys[];
+  uint16_t* idx = (uint16_t*)(keys + P);
+  int* iscr = (int*)(idx + P + 8);
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d) * ld;
+  double* y = Y + (f * D + d) * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  int nrow_l = 0, nv_l = 0;
+  for (int i = threadIdx.x; i < P; i += CS_NT) {
+    uint64_t k = KEY_SENTINEL;
+    uint16_t id = 0xffff;
+    if (i < A) {
+      bool p = prow ? prow[i] != 0 : true;
+      if (p) {
+        double t = x[i];
+        nrow_l += 1;
+        if (t == t) { k = okey(t); id = (uint16_t)i; nv_l += 1; }
+      }
+    }
+    keys[i] = k;
+    idx[i] = id;
+  }
+  int nrow, nv;
+  block_exscan<CS_NT>(nrow_l, iscr, &nrow);
+  block_exscan<CS_NT>(nv_l, iscr, &nv);
+  // NaN / absent rows are written here (sorted members are written below)
+  for (int64_t a = threadIdx.x; a < A; a += CS_NT) {
+    bool p = prow ? prow[a] != 0 : true;
+    if (!p) y[a] = qnan();
+    else if (!(x[a] == x[a])) y[a] = (nrow == 1) ? 0.5 : qnan();
+  }
+  bitonic_sort<CS_NT>(keys, idx, P);
+  // dense ranks need the number of distinct keys before each position
+  int* dstart = nullptr;
+  if (method == FMX_RANK_DENSE) {
+    // chunked scan of group-start flags
+    const int C = (nv + CS_NT - 1) / CS_NT;
+    const int p0 = threadIdx.x * C, p1 = min(nv, p0 + C);
+    int c = 0;
+    for (int p = p0; p < p1; ++p) c += (p == 0 || keys[p] != keys[p - 1]);
+    int tot;
+    int base = block_exscan<CS_NT>(c, iscr, &tot);
+    // store dense rank (1-based) of each position into the upper half of an int view of
+    // the key array is not possible (keys still needed) -> recompute on the fly below
+    dstart = iscr;  // unused marker
+    for (int p = p0; p < p1; ++p) {
+      base += (p == 0 || keys[p] != keys[p - 1]);
+      double r = (double)base;
+      int a = idx[p];
+      y[a] = (nrow == 1) ? 0.5 : (r - 1.0) / (double)(nrow - 1);
+    }
+    return;
+  }
+  (void)dstart;
+  for (int p = threadIdx.x; p < nv; p += CS_NT) {
+    uint64_t k = keys[p];
+    int less = lower_bound_u64(keys, 0, p + 1, k);
+    int eq = upper_bound_u64(keys, p, nv, k) - less;
+    double r;
+    switch (method) {
+      case FMX_RANK_MIN: r = (double)(less + 1); break;
+      case FMX_RANK_MAX: r = (double)(less + eq); break;
+      case FMX_RANK_FIRST: r = (double)(p + 1); break;
+      default: r = (double)less + (double)(eq + 1) / 2.0;
+    }
+    int a = idx[p];
+    y[a] = (nrow == 1) ? 0.5 : (r - 1.0) / (double)(nrow - 1);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// cs_winsor (OP 0) / cs_filter_center (OP 1): numpy linear percentiles of the non-NaN
+// values (pandas Series.quantile -> np.percentile(q*100) / 100).
+template <int OP>
+__global__ void __launch_bounds__(CS_NT)
+k_cs_quantile(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+              int P, double qlo, double qhi, const uint8_t* __restrict__ present) {
+  extern __shared__ uint64_t keys[];
+  uint16_t* idx = (uint16_t*)(keys + P);
+  int* iscr = (int*)(idx + P + 8);
+  double* qv = (double*)(iscr + 16);
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d) * ld;
+  double* y = Y + (f * D + d) * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  int nv_l = 0;
+  for (int i = threadIdx.x; i < P; i += CS_NT) {
+    uint64_t k = KEY_SENTINEL;
+    if (i < A && (prow ? prow[i] != 0 : true)) {
+      double t = x[i];
+      if (t == t) { k = okey(t); nv_l += 1; }
+    }
+    keys[i] = k;
+    idx[i] = (uint16_t)i;
+  }
+  int nv;
+  block_exscan<CS_NT>(nv_l, iscr, &nv);
+  bitonic_sort<CS_NT>(keys, idx, P);
+  if (threadIdx.x == 0) {
+    if (nv > 0) {
+      qv[0] = sorted_percentile(keys, nv, qlo);
+      qv[1] = sorted_percentile(keys, nv, qhi);
+    } else {
+      qv[0] = qv[1] = qnan();
+    }
+  }
+  __syncthreads();
+  const double lo = qv[0], hi = qv[1];
+  for (int64_t a = threadIdx.x; a < A; a += CS_NT) {
+    bool p = prow ? prow[a] != 0 : true;
+    if (!p) { y[a] = qnan(); continue; }
+    double t = x[a];
+    double o;
+    if (OP == 0) {
+      o = t;
+      if (nv >= 5) o = (t < lo) ? lo : ((t > hi) ? hi : t);
+    } else {
+      o = (t < lo || t > hi) ? t : 0.0;
+    }
+    y[a] = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Group ops per (date, group): G[d][a] holds dense group ids (-1 = NaN group, dropped by
+// the reference's groupby).  Elements are sorted by (group, key, asset); each group's
+// members are then contiguous and in asset order for the pairwise sums.
+template <int OP>
+__global__ void __launch_bounds__(CS_NT)
+k_group(const double* __restrict__ X, const int32_t* __restrict__ G, double* __restrict__ Y, int64_t D,
+        int64_t A, int64_t ld, int P, int ngroups, int method, const uint8_t* __restrict__ present,
+        PwTable pw) {
+  extern __shared__ uint64_t keys[];
+  uint16_t* idx = (uint16_t*)(keys + P);
+  uint16_t* grp = idx + P;
+  double* vals = (double*)(((uintptr_t)(grp + P) + 15) & ~(uintptr_t)15);  // [P] values in sorted order
+  double* nodes = vals + P;                                              // [2P/64 + 8]
+  int* iscr = (int*)(nodes + (2 * (P / 64) + 8));
+  int* gbound = iscr + 16;                                               // [ngroups+1]
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d) * ld;
+  const int32_t* g = G + d * ld;
+  double* y = Y + (f * D + d) * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  const bool by_value = (OP == 3);
+  for (int i = threadIdx.x; i < P; i += CS_NT) {
+    uint64_t k = KEY_SENTINEL;
+    uint16_t gi = 0xffff;
+    if (i < A && (prow ? prow[i] != 0 : true)) {
+      int gg = g[i];
+      if (gg >= 0) {
+        gi = (uint16_t)gg;
+        double t = x[i];
+        k = by_value ? (t == t ? okey(t) : KEY_SENTINEL - 1) : 0;
+      }
+    }
+    keys[i] = k;
+    idx[i] = (uint16_t)i;
+    grp[i] = gi;
+  }
+  // rows outside any group -> NaN
+  for (int64_t a = threadIdx.x; a < A; a += CS_NT) {
+    bool p = prow ? prow[a] != 0 : true;
+    if (!p || g[a] < 0) y[a] = qnan();
+  }
+  bitonic_sort_grp<CS_NT>(keys, idx, grp, P);
+  for (int i = threadIdx.x; i < P; i += CS_NT) vals[i] = (grp[i] != 0xffff) ? x[idx[i]] : 0.0;
+  // group boundaries
+  for (int gg = threadIdx.x; gg <= ngroups; gg += CS_NT) {
+    int lo = 0, hi = P;
+    while (lo < hi) { int m = (lo + hi) >> 1; if (grp[m] < gg) lo = m + 1; else hi = m; }
+    gbound[gg] = lo;
+  }
+  __syncthreads();
+  for (int gg = 0; gg < ngroups; ++gg) {
+    const int s = gbound[gg], e = gbound[gg + 1], n = e - s;
+    if (n == 0) continue;
+    if (OP == 3) {
+      // rank over non-NaN members (keys < SENTINEL-1); NaN members sort last in the group
+      int nvl = 0;
+      for (int p = s + threadIdx.x; p < e; p += CS_NT) nvl += keys[p] < KEY_SENTINEL - 1;
+      int nvv;
+      block_exscan<CS_NT>(nvl, iscr, &nvv);
+      for (int p = s + threadIdx.x; p < e; p += CS_NT) {
+        int a = idx[p];
+        if (nvv <= 1) { y[a] = 0.5; continue; }
+        uint64_t k = keys[p];
+        if (!(k < KEY_SENTINEL - 1)) { y[a] = qnan(); continue; }
+        int less = lower_bound_u64(keys, s, p + 1, k) - s;
+        int eq = upper_bound_u64(keys, p, s + nvv, k) - (less + s);
+        double r;
+        switch (method) {
+          case FMX_RANK_MIN: r = (double)(less + 1); break;
+          case FMX_RANK_MAX: r = (double)(less + eq); break;
+          case FMX_RANK_FIRST: r = (double)(p - s + 1); break;
+          default: r = (double)less + (double)(eq + 1) / 2.0;
+        }
+        y[a] = (r - 1.0) / (double)(nvv - 1);
+      }
+      continue;
+    }
+    const double* vg = vals + s;
+    int cl = 0;
+    for (int i = threadIdx.x; i < n; i += CS_NT) cl += vg[i] == vg[i];
+    int cnt;
+    block_exscan<CS_NT>(cl, iscr, &cnt);
+    const int32_t* sch = pw.get(n);
+    double s1 = block_pw_sum<CS_NT>([&](int i) { double t = vg[i]; return t == t ? t : 0.0; }, sch, nodes);
+    double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+    double sd = 0.0;
+    if (OP == 2) {
+      double s2 = block_pw_sum<CS_NT>([&](int i) {
+        double t = vg[i];
+        double z = t == t ? t : 0.0;
+        double q = (mean - z) * (mean - z);
+        return t == t ? q : 0.0;
+      }, sch, nodes);
+      sd = sqrt(cnt > 0 ? s2 / (double)cnt : qnan());
+    }
+    const bool guard = (OP == 2) && (sd == 0.0 || sd != sd);
+    for (int i = threadIdx.x; i < n; i += CS_NT) {
+      double t = vg[i];
+      double o;
+      if (OP == 0) o = mean;
+      else if (OP == 1) o = t - mean;
+      else o = guard ? 0.0 : (t - mean) / sd;
+      y[idx[s + i]] = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// cs_regression: per date OLS on pair-valid rows (population moments, pandas means).
+__global__ void __launch_bounds__(CS_NT)
+k_cs_regression(const double* __restrict__ Yv, const double* __restrict__ Xv, double* __restrict__ Out,
+                int64_t D, int64_t A, int64_t ld, int rettype, const uint8_t* __restrict__ present,
+                PwTable pw) {
+  extern __shared__ double lds[];
+  double* xs = lds;            // [A]
+  double* ys = xs + A;         // [A]
+  uint16_t* pos = (uint16_t*)(ys + A);
+  double* nodes = (double*)((char*)pos + ((A * 2 + 15) & ~15));
+  int* iscr = (int*)(nodes + (2 * (A / 64) + 8));
+  const int64_t d = blockIdx.x;
+  const double* x = Xv + d * ld;
+  const double* yv = Yv + d * ld;
+  double* o = Out + d * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  // compact pair-valid rows in asset order
+  const int64_t C = (A + CS_NT - 1) / CS_NT;
+  const int64_t a0 = threadIdx.x * C, a1 = min<int64_t>(A, a0 + C);
+  int cnt = 0;
+  for (int64_t a = a0; a < a1; ++a) {
+    bool ok = (prow ? prow[a] != 0 : true) && x[a] == x[a] && yv[a] == yv[a];
+    cnt += ok;
+  }
+  int n;
+  int base = block_exscan<CS_NT>(cnt, iscr, &n);
+  for (int64_t a = a0; a < a1; ++a) {
+    bool ok = (prow ? prow[a] != 0 : true) && x[a] == x[a] && yv[a] == yv[a];
+    if (ok) { xs[base] = x[a]; ys[base] = yv[a]; pos[base] = (uint16_t)a; ++base; }
+    o[a] = qnan();
+  }
+  __syncthreads();
+  if (n < 2) return;
+  const int32_t* sch = pw.get(n);
+  const double dn = (double)n;
+  double mx = block_pw_sum<CS_NT>([&](int i) { return xs[i]; }, sch, nodes) / dn;
+  double my = block_pw_sum<CS_NT>([&](int i) { return ys[i]; }, sch, nodes) / dn;
+  double cov = block_pw_sum<CS_NT>([&](int i) { return (xs[i] - mx) * (ys[i] - my); }, sch, nodes) / dn;
+  double var_x = block_pw_sum<CS_NT>([&](int i) { double t = xs[i] - mx; return t * t; }, sch, nodes) / dn;
+  double beta = cov / var_x;
+  double alpha = my - beta * mx;
+  double r2 = 0.0;
+  if (rettype == 4) {
+    double var_y = block_pw_sum<CS_NT>([&](int i) { double t = ys[i] - my; return t * t; }, sch, nodes) / dn;
+    r2 = (cov * cov) / (var_x * var_y);
+  }
+  for (int i = threadIdx.x; i < n; i += CS_NT) {
+    double fitted = alpha + beta * xs[i];
+    double r;
+    switch (rettype) {
+      case 0: r = ys[i] - fitted; break;   // resid
+      case 1: r = beta; break;
+      case 2: r = alpha; break;
+      case 3: r = fitted; break;
+      default: r = r2;
+    }
+    o[pos[i]] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Elementwise (operations.py:80-101) and bucket codes (pd.cut, :104-110).
+__global__ void k_elementwise(const double* __restrict__ X, double* __restrict__ Y, int64_t n, int op,
+                              double a, double b) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    double v = X[i], o;
+    switch (op) {
+      case FMX_EW_SIGN: o = (v > 0) ? 1.0 : ((v < 0) ? -1.0 : (v == v ? 0.0 : v)); break;  // np.sign(-0.) = +0.
+      case FMX_EW_POWER:
+        // ndarray.__pow__ fast paths (numpy fast_scalar_power), reached via Series.__pow__
+        if (a == 2.0) o = v * v;
+        else if (a == 0.5) o = sqrt(v);
+        else if (a == 1.0) o = v;
+        else if (a == -1.0) o = 1.0 / v;
+        else if (a == 0.0) o = 1.0;
+        else o = pow(v, a);
+        break;
+      case FMX_EW_LOG: o = log(v); break;
+      case FMX_EW_ABS: o = fabs(v); break;
+      case FMX_EW_CLIP: o = (v < a) ? a : ((v > b) ? b : v); break;
+      case FMX_EW_WHERE: o = (v != 0.0) ? a : b; break;   // cond as 0/1 (NaN -> true)
+      default: o = v;
+    }
+    Y[i] = o;
+  }
+}
+
+__global__ void k_bucket(const double* __restrict__ X, int32_t* __restrict__ codes, int64_t n,
+                         const double* __restrict__ edges, int ne) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    double v = X[i];
+    int c = -1;
+    if (v == v) {
+      // searchsorted(edges, v, side='left')
+      int lo = 0, hi = ne;
+      while (lo < hi) { int m = (lo + hi) >> 1; if (edges[m] < v) lo = m + 1; else hi = m; }
+      int id = (v == edges[0]) ? 1 : lo;
+      if (id > 0 && id <= ne - 1) c = id - 1;
+    }
+    codes[i] = c;
+  }
+}
+
+static fmx_status set_lds(const void* k, size_t lds) {
+  if (lds > 160 * 1024) {
+    set_error("row too long for the LDS-resident cross-sectional kernels (" + std::to_string(lds) + " B)");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return FMX_OK;
+}
+
+}  // namespace fmx
+
+using namespace fmx;
+
+extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
+                                    int64_t ld, const uint8_t* present, void* stream) {
+  FMX_ARG(X && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_MARKET_NEUTRALIZE, "unknown cs op");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  size_t lds = A * 8 + (present ? ((A * 2 + 15) & ~15) : 0) + (2 * (A / 64) + 8) * 8 + 16 * 4 + 64;
+  const void* k = op == FMX_CS_ZSCORE ? (const void*)k_cs_moment<FMX_CS_ZSCORE>
+                : op == FMX_CS_MEAN ? (const void*)k_cs_moment<FMX_CS_MEAN>
+                                    : (const void*)k_cs_moment<FMX_CS_MARKET_NEUTRALIZE>;
+  if ((e = set_lds(k, lds))) return e;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(CS_NT), args, lds, as_stream(stream)));
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                  int32_t method, const uint8_t* present, void* stream) {
+  FMX_ARG(X && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(method >= FMX_RANK_AVERAGE && method <= FMX_RANK_DENSE, "unknown rank method");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  int P = next_pow2((int)A);
+  if (P < 2) P = 2;
+  size_t lds = (size_t)P * 10 + 16 + 16 * 4 + 64;
+  fmx_status e;
+  if ((e = set_lds((const void*)k_cs_rank, lds))) return e;
+  int m = method;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&P, (void*)&m, (void*)&present};
+  FMX_HIP(hipLaunchKernel((const void*)k_cs_rank, dim3((unsigned)D, (unsigned)F), dim3(CS_NT), args, lds,
+                          as_stream(stream)));
+  return FMX_OK;
+}
+
+static fmx_status cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                              double qlo, double qhi, const uint8_t* present, void* stream) {
+  FMX_ARG(X && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  int P = next_pow2((int)A);
+  if (P < 2) P = 2;
+  size_t lds = (size_t)P * 10 + 16 + 16 * 4 + 16 + 64;
+  const void* k = op == 0 ? (const void*)k_cs_quantile<0> : (const void*)k_cs_quantile<1>;
+  fmx_status e;
+  if ((e = set_lds(k, lds))) return e;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&P, (void*)&qlo, (void*)&qhi,
+                  (void*)&present};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(CS_NT), args, lds, as_stream(stream)));
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                    double qlo, double qhi, const uint8_t* present, void* stream) {
+  return cs_quantile(0, X, Y, F, D, A, ld, qlo, qhi, present, stream);
+}
+
+extern "C" fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D, int64_t A,
+                                           int64_t ld, double qlo, double qhi, const uint8_t* present,
+                                           void* stream) {
+  return cs_quantile(1, X, Y, F, D, A, ld, qlo, qhi, present, stream);
+}
+
+extern "C" fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F,
+                                   int64_t D, int64_t A, int64_t ld, int32_t ngroups, int32_t method,
+                                   const uint8_t* present, void* stream) {
+  FMX_ARG(X && G && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(op >= FMX_GROUP_MEAN && op <= FMX_GROUP_RANK, "unknown group op");
+  FMX_ARG(ngroups >= 0 && ngroups < 65535, "bad group count");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  int P = next_pow2((int)A);
+  if (P < 2) P = 2;
+  size_t lds = (size_t)P * 12 + 16 + (size_t)P * 8 + (2 * (P / 64) + 8) * 8 + 16 * 4 + (ngroups + 1) * 4 + 64;
+  const void* k = op == FMX_GROUP_MEAN ? (const void*)k_group<0>
+                : op == FMX_GROUP_NEUTRALIZE ? (const void*)k_group<1>
+                : op == FMX_GROUP_NORMALIZE ? (const void*)k_group<2>
+                                            : (const void*)k_group<3>;
+  if ((e = set_lds(k, lds))) return e;
+  int ng = ngroups, m = method;
+  void* args[] = {(void*)&X, (void*)&G, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&P, (void*)&ng,
+                  (void*)&m, (void*)&present, (void*)&pw};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(CS_NT), args, lds, as_stream(stream)));
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_cs_regression(const double* Yv, const double* Xv, double* Out, int64_t D, int64_t A,
+                                        int64_t ld, int32_t rettype, const uint8_t* present, void* stream) {
+  FMX_ARG(Yv && Xv && Out, "null panel");
+  FMX_ARG(D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(rettype >= 0 && rettype <= 4, "rettype");
+  if (D == 0 || A == 0) return FMX_OK;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  size_t lds = (size_t)A * 16 + ((A * 2 + 15) & ~15) + (2 * (A / 64) + 8) * 8 + 16 * 4 + 64;
+  if ((e = set_lds((const void*)k_cs_regression, lds))) return e;
+  int rt = rettype;
+  void* args[] = {(void*)&Yv, (void*)&Xv, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld, (void*)&rt,
+                  (void*)&present, (void*)&pw};
+  FMX_HIP(hipLaunchKernel((const void*)k_cs_regression, dim3((unsigned)D), dim3(CS_NT), args, lds,
+                          as_stream(stream)));
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_elementwise(int32_t op, const double* X, double* Y, int64_t n, double a, double b,
+                                      void* stream) {
+  FMX_ARG(X && Y && n >= 0, "bad args");
+  FMX_ARG(op >= FMX_EW_SIGN && op <= FMX_EW_WHERE, "unknown elementwise op");
+  if (n == 0) return FMX_OK;
+  int grid = (int)std::min<int64_t>(ceil_div(n, 256), 8192);
+  k_elementwise<<<grid, 256, 0, as_stream(stream)>>>(X, Y, n, op, a, b);
+  FMX_LAUNCH_CHECK("k_elementwise");
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_bucket(const double* X, int32_t* codes, int64_t n, const double* edges,
+                                 int32_t n_edges, void* stream) {
+  FMX_ARG(X && codes && edges && n >= 0 && n_edges >= 2, "bad args");
+  if (n == 0) return FMX_OK;
+  int grid = (int)std::min<int64_t>(ceil_div(n, 256), 8192);
+  k_bucket<<<grid, 256, 0, as_stream(stream)>>>(X, codes, n, edges, n_edges);
+  FMX_LAUNCH_CHECK("k_bucket");
+  return FMX_OK;
+}

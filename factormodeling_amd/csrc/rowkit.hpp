@@ -1,0 +1,246 @@
+// Block-level building blocks for per-row (cross-sectional) kernels.
+//
+// * block_pw_sum: numpy's float64 pairwise summation (add.reduce), bit-for-bit, driven by
+//   a host-built schedule for the row length n (see pw_schedule in capi.hip).  pandas'
+//   nanmean/nanvar (Series.mean()/.std()) sum with it, so reproducing its tree makes the
+//   cross-sectional moments bit-identical to the reference.
+// * block_exscan: exclusive prefix sum of one int per thread.
+// * bitonic sort of (uint64 key, uint16 idx) pairs in LDS, ordered by (key, idx) so that
+//   ties come out in position order (pandas method='first' / stable ordering).
+#pragma once
+
+#include "fmx_common.hpp"
+
+namespace fmx {
+
+// Schedule blob layout (int32):
+//   [0] n  [1] L (#leaves, 0 => n < 8: sequential from 0)  [2] I (#internal nodes)
+//   [3] R (#combine rounds)  [4] root node id
+//   [5 .. 5+L)            leaf start
+//   [5+L .. 5+2L)         leaf length
+//   [5+2L .. 5+2L+R+1)    round offsets into the triple list
+//   [.. + 3I)             (dst, left, right) node triples, grouped by round
+struct PwView {
+  const int32_t* b;
+  __device__ int n() const { return b[0]; }
+  __device__ int L() const { return b[1]; }
+  __device__ int I() const { return b[2]; }
+  __device__ int R() const { return b[3]; }
+  __device__ int root() const { return b[4]; }
+  __device__ int lstart(int k) const { return b[5 + k]; }
+  __device__ int llen(int k) const { return b[5 + L() + k]; }
+  __device__ int roff(int r) const { return b[5 + 2 * L() + r]; }
+  __device__ const int32_t* trip() const { return b + 5 + 2 * L() + R() + 1; }
+};
+
+// nodes: LDS scratch of >= 2L doubles (+1).  Returns the sum to every thread.
+template <int NT, class Elem>
+__device__ double block_pw_sum(Elem elem, const int32_t* __restrict__ sched, double* nodes) {
+  PwView s{sched};
+  const int L = s.L();
+  const int tid = threadIdx.x;
+  if (L == 0) {
+    if (tid == 0) {
+      double r = 0.0;
+      const int n = s.n();
+      for (int i = 0; i < n; ++i) r += elem(i);
+      nodes[0] = r;
+    }
+    __syncthreads();
+    double r = nodes[0];
+    __syncthreads();
+    return r;
+  }
+  for (int t0 = 0; t0 < L * 8; t0 += NT) {
+    const int t = t0 + tid;
+    const bool act = t < L * 8;
+    const int leaf = t >> 3, j = t & 7;
+    double r = 0.0;
+    int st = 0, len = 0, stop = 0;
+    if (act) {
+      st = s.lstart(leaf);
+      len = s.llen(leaf);
+      stop = len - (len & 7);
+      r = elem(st + j);
+      for (int i = 8; i < stop; i += 8) r += elem(st + i + j);
+    }
+    // ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) as an xor butterfly (IEEE + commutes)
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (act && j == 0) {
+      for (int i = stop; i < len; ++i) r += elem(st + i);
+      nodes[leaf] = r;
+    }
+  }
+  __syncthreads();
+  const int R = s.R();
+  const int32_t* tr = s.trip();
+  for (int rr = 0; rr < R; ++rr) {
+    for (int q = s.roff(rr) + tid; q < s.roff(rr + 1); q += NT) {
+      nodes[tr[3 * q]] = nodes[tr[3 * q + 1]] + nodes[tr[3 * q + 2]];
+    }
+    __syncthreads();
+  }
+  double r = nodes[s.root()];
+  __syncthreads();
+  return r;
+}
+
+// Exclusive scan of v across the block; *total receives the sum.  scratch: NT/64 ints.
+template <int NT>
+__device__ int block_exscan(int v, int* scratch, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) scratch[wid] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < NT / 64; ++w) {
+    int x = scratch[w];
+    if (w < wid) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+template <int NT>
+__device__ double block_sum(double v, double* scratch) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < NT / 64; ++w) t += scratch[w];
+  __syncthreads();
+  return t;
+}
+
+template <int NT>
+__device__ double block_max(double v, double* scratch) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double t = scratch[0];
+  for (int w = 1; w < NT / 64; ++w) t = fmax(t, scratch[w]);
+  __syncthreads();
+  return t;
+}
+
+template <int NT>
+__device__ double block_min(double v, double* scratch) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double t = scratch[0];
+  for (int w = 1; w < NT / 64; ++w) t = fmin(t, scratch[w]);
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ bool kv_greater(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
+  return ka > kb || (ka == kb && ia > ib);
+}
+
+// Bitonic sort of P (power of two) (key, idx) pairs in LDS, ascending by (key, idx).
+template <int NT>
+__device__ void bitonic_sort(uint64_t* key, uint16_t* idx, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += NT) {
+        const int i = 2 * t - (t & (j - 1));
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        uint64_t a = key[i], b = key[l];
+        uint16_t ia = idx[i], ib = idx[l];
+        bool gt = kv_greater(a, ia, b, ib);
+        if (gt == up) {
+          key[i] = b; key[l] = a;
+          idx[i] = ib; idx[l] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Bitonic sort with a 16-bit group as the primary key: (grp, key, idx).
+template <int NT>
+__device__ void bitonic_sort_grp(uint64_t* key, uint16_t* idx, uint16_t* grp, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += NT) {
+        const int i = 2 * t - (t & (j - 1));
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        uint64_t a = key[i], b = key[l];
+        uint16_t ia = idx[i], ib = idx[l], ga = grp[i], gb = grp[l];
+        bool gt = ga > gb || (ga == gb && kv_greater(a, ia, b, ib));
+        if (gt == up) {
+          key[i] = b; key[l] = a;
+          idx[i] = ib; idx[l] = ia;
+          grp[i] = gb; grp[l] = ga;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// first index p in [lo, hi) with key[p] >= k  /  > k
+__device__ __forceinline__ int lower_bound_u64(const uint64_t* key, int lo, int hi, uint64_t k) {
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if (key[m] < k) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+__device__ __forceinline__ int upper_bound_u64(const uint64_t* key, int lo, int hi, uint64_t k) {
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if (key[m] <= k) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// numpy percentile(method='linear') on the first n ascending sorted keys at fraction q.
+__device__ __forceinline__ double sorted_percentile(const uint64_t* key, int n, double q) {
+  double vi = (double)(n - 1) * q;
+  double a, b, g;
+  if (vi >= (double)(n - 1)) {
+    a = b = okey_inv(key[n - 1]);
+    g = vi + 1.0;
+  } else {
+    double pf = floor(vi);
+    int p = (int)pf;
+    g = vi - pf;
+    a = okey_inv(key[p]);
+    b = okey_inv(key[p + 1]);
+  }
+  double diff = b - a;
+  return (g >= 0.5) ? b - diff * (1.0 - g) : a + diff * g;
+}
+
+inline int next_pow2(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// Device view of the cached schedules for every row length n <= nmax.
+struct PwTable {
+  const int32_t* off;   // [nmax + 1]
+  const int32_t* blob;
+  __device__ const int32_t* get(int n) const { return blob + off[n]; }
+};
+// Host: schedule table covering every n <= nmax on the current device (capi.hip).
+PwTable pw_table(int nmax, fmx_status* err);
+
+}  // namespace fmx

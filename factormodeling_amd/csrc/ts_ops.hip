@@ -1,0 +1,489 @@
+// Time-series (per-symbol rolling) kernels.
+//
+// Reference: operations.py:6-51 (ts_sum/mean/std/zscore/rank/diff/delay/decay/backfill),
+// operations.py:185-246 (ts_regression_fast rolling moments) and the builder-defined
+// ts_corr (pandas Rolling.corr semantics).  The reference runs
+// ``series.groupby(level='symbol').transform(lambda x: x.rolling(w).<agg>())``: a
+// sequential walk over each symbol's rows.  Here one lane owns one (factor, asset)
+// column of the [F][D][ld] panel and walks its dates; at each date the 64 lanes of a
+// wave read 64 consecutive assets (coalesced 512-B rows).
+//
+// The window history is a thread-private ring in LDS laid out ring[slot*64 + lane]
+// (bank-conflict free, no barriers).  Rows whose presence byte is 0 are skipped: the
+// ring only advances on present rows, which reproduces the reference's row-based
+// windows on ragged panels.
+//
+// The add/remove state machines replicate pandas 2.3.3 _libs/window/aggregations.pyx
+// (roll_sum / roll_mean / roll_var incl. Kahan compensation, the consecutive-same-
+// value guard and zsqrt), so with -ffp-contract=off the outputs are bit-identical to
+// pandas.
+#include "fmx_common.hpp"
+
+namespace fmx {
+
+constexpr int TS_BLOCK = 64;   // one wave per block: the LDS ring is thread-private
+constexpr int TS_UNROLL = 8;   // dates prefetched per lane
+
+struct SumSt {
+  double s, ca, cr, prev;
+  int64_t n, same;
+  __device__ void init(double first) { s = ca = cr = 0.0; n = 0; same = 0; prev = first; }
+  __device__ void add(double v) {
+    if (v == v) {
+      n += 1;
+      double y = v - ca, t = s + y;
+      ca = t - s - y; s = t;
+      if (v == prev) same += 1; else same = 1;
+      prev = v;
+    }
+  }
+  __device__ void remove(double v) {
+    if (v == v) {
+      n -= 1;
+      double y = -v - cr, t = s + y;
+      cr = t - s - y; s = t;
+    }
+  }
+  __device__ double result(int64_t minp) const {
+    if (n == 0 && minp == 0) return 0.0;
+    if (n >= minp) return (same >= n) ? prev * (double)n : s;
+    return qnan();
+  }
+};
+
+struct MeanSt {
+  double s, ca, cr, prev;
+  int64_t n, neg, same;
+  __device__ void init(double first) { s = ca = cr = 0.0; n = neg = same = 0; prev = first; }
+  __device__ void add(double v) {
+    if (v == v) {
+      n += 1;
+      double y = v - ca, t = s + y;
+      ca = t - s - y; s = t;
+      if (__builtin_signbit(v)) neg += 1;
+      if (v == prev) same += 1; else same = 1;
+      prev = v;
+    }
+  }
+  __device__ void remove(double v) {
+    if (v == v) {
+      n -= 1;
+      double y = -v - cr, t = s + y;
+      cr = t - s - y; s = t;
+      if (__builtin_signbit(v)) neg -= 1;
+    }
+  }
+  __device__ double result(int64_t minp) const {
+    if (n >= minp && n > 0) {
+      double r = s / (double)n;
+      if (same >= n) r = prev;
+      else if (neg == 0 && r < 0) r = 0.0;
+      else if (neg == n && r > 0) r = 0.0;
+      return r;
+    }
+    return qnan();
+  }
+};
+
+struct VarSt {
+  double mean, ssq, n, ca, cr, prev;
+  int64_t same;
+  __device__ void init(double first) { mean = ssq = n = ca = cr = 0.0; same = 0; prev = first; }
+  __device__ void add(double v) {
+    if (v != v) return;
+    n += 1.0;
+    if (v == prev) same += 1; else same = 1;
+    prev = v;
+    double pm = mean - ca;
+    double y = v - ca;
+    double t = y - mean;
+    ca = t + mean - y;
+    if (n != 0.0) mean = mean + t / n; else mean = 0.0;
+    ssq = ssq + (v - pm) * (v - mean);
+  }
+  __device__ void remove(double v) {
+    if (v == v) {
+      n -= 1.0;
+      if (n != 0.0) {
+        double pm = mean - cr;
+        double y = v - cr;
+        double t = y - mean;
+        cr = t + mean - y;
+        mean = mean - t / n;
+        ssq = ssq - (v - pm) * (v - mean);
+      } else {
+        mean = 0.0;
+        ssq = 0.0;
+      }
+    }
+  }
+  __device__ double var(int64_t minp, int ddof) const {
+    if (minp < 1) minp = 1;
+    if (n >= (double)minp && n > (double)ddof) {
+      if (n == 1.0 || (double)same >= n) return 0.0;
+      return ssq / (n - (double)ddof);
+    }
+    return qnan();
+  }
+};
+
+__device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v); }
+
+// ------------------------------------------------------------------------------------
+// Generic walker: calls body(d, v) for each present row of the lane's column, with up
+// to TS_UNROLL loads in flight.
+template <class Body>
+__device__ __forceinline__ void walk_column(const double* __restrict__ x, double* __restrict__ y,
+                                            int64_t D, int64_t ld, const uint8_t* __restrict__ pres,
+                                            Body&& body) {
+  for (int64_t d0 = 0; d0 < D; d0 += TS_UNROLL) {
+    double v[TS_UNROLL];
+    uint8_t p[TS_UNROLL];
+#pragma unroll
+    for (int u = 0; u < TS_UNROLL; ++u) {
+      int64_t d = d0 + u;
+      if (d < D) {
+        v[u] = x[d * ld];
+        p[u] = pres ? pres[d * ld] : 1;
+      } else {
+        p[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TS_UNROLL; ++u) {
+      int64_t d = d0 + u;
+      if (d < D) {
+        if (p[u]) y[d * ld] = body(d, v[u]);
+        else y[d * ld] = qnan();
+      }
+    }
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(TS_BLOCK)
+k_ts(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+     int W, const uint8_t* __restrict__ present) {
+  extern __shared__ double ring[];  // [W][TS_BLOCK]
+  const int lane = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+  if (a >= A) return;
+  const int64_t f = blockIdx.y;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  const uint8_t* pres = present ? present + a : nullptr;
+
+  int64_t i = 0;  // present-row counter
+  int slot = 0;
+  int nan_in_win = 0;
+  SumSt ss; MeanSt ms; VarSt vs; double last = qnan();
+  bool first = true;
+
+  walk_column(x, y, D, ld, pres, [&](int64_t d, double v) -> double {
+    (void)d;
+    if (first) { ss.init(v); ms.init(v); vs.init(v); first = false; }
+    double old = qnan();
+    if (OP != FMX_TS_BACKFILL) {
+      if (i >= W) old = ring[slot * TS_BLOCK + lane];
+      ring[slot * TS_BLOCK + lane] = v;
+      slot = (slot + 1 == W) ? 0 : slot + 1;
+    }
+    double out;
+    if (OP == FMX_TS_SUM) {
+      if (i >= W) ss.remove(old);
+      ss.add(v);
+      out = ss.result(W);
+    } else if (OP == FMX_TS_MEAN) {
+      if (i >= W) ms.remove(old);
+      ms.add(v);
+      out = ms.result(W);
+    } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
+      if (i >= W) vs.remove(old);
+      vs.add(v);
+      double var = vs.var(W, 1);
+      out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
+    } else if (OP == FMX_TS_ZSCORE) {
+      if (i >= W) { ms.remove(old); vs.remove(old); }
+      ms.add(v); vs.add(v);
+      double m = ms.result(W);
+      double s = zsqrt(vs.var(W, 1));
+      if (s == 0.0) s = qnan();
+      out = (v - m) / s;
+    } else if (OP == FMX_TS_RANK || OP == FMX_TS_DECAY) {
+      if (i >= W && old != old) nan_in_win -= 1;
+      if (v != v) nan_in_win += 1;
+      if (i + 1 < W || nan_in_win > 0) {
+        out = qnan();
+      } else if (OP == FMX_TS_RANK) {
+        int less = 0, eq = 0;
+        for (int k = 0; k < W; ++k) {
+          double u = ring[k * TS_BLOCK + lane];
+          less += (u < v);
+          eq += (u == v);
+        }
+        out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
+      } else {
+        // oldest element sits at `slot` (just advanced); weights 1..W oldest->newest
+        double acc = 0.0;
+        int s = slot;
+        for (int k = 1; k <= W; ++k) {
+          acc += ring[s * TS_BLOCK + lane] * (double)k;
+          s = (s + 1 == W) ? 0 : s + 1;
+        }
+        out = acc / ((double)W * (double)(W + 1) / 2.0);
+      }
+    } else if (OP == FMX_TS_DIFF) {
+      out = (i >= W) ? v - old : qnan();
+    } else if (OP == FMX_TS_DELAY) {
+      out = (i >= W) ? old : qnan();
+    } else {  // BACKFILL
+      if (v == v) last = v;
+      out = last;
+    }
+    i += 1;
+    return out;
+  });
+}
+
+// W == 0: diff -> x - x, delay -> x, decay -> x (no ring).
+__global__ void k_ts_window0(const double* __restrict__ X, double* __restrict__ Y, int64_t n_total,
+                             int op, const uint8_t* __restrict__ present, int64_t DA, int64_t ld) {
+  (void)ld;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n_total; i += stride) {
+    double v = X[i];
+    bool p = present ? present[i % DA] : true;
+    double o = (op == FMX_TS_DIFF) ? v - v : v;
+    Y[i] = p ? o : qnan();
+  }
+}
+
+// Negative window for diff/delay: a lead by K=-W present rows.  Each row first gets NaN
+// and is overwritten once the row K steps ahead arrives.
+template <int OP>
+__global__ void __launch_bounds__(TS_BLOCK)
+k_ts_lead(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+          int K, const uint8_t* __restrict__ present) {
+  extern __shared__ double ring[];  // values [K][64] then positions [K][64]
+  double* rpos = ring + (int64_t)K * TS_BLOCK;
+  const int lane = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+  if (a >= A) return;
+  const int64_t f = blockIdx.y;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  int64_t i = 0;
+  int slot = 0;
+  for (int64_t d = 0; d < D; ++d) {
+    bool p = present ? present[d * ld + a] != 0 : true;
+    y[d * ld] = qnan();
+    if (!p) continue;
+    double v = x[d * ld];
+    if (i >= K) {
+      double ov = ring[slot * TS_BLOCK + lane];
+      int64_t od = (int64_t)rpos[slot * TS_BLOCK + lane];
+      y[od * ld] = (OP == FMX_TS_DIFF) ? ov - v : v;
+    }
+    ring[slot * TS_BLOCK + lane] = v;
+    rpos[slot * TS_BLOCK + lane] = (double)d;
+    slot = (slot + 1 == K) ? 0 : slot + 1;
+    i += 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// ts_corr (builder-defined; pandas Rolling.corr): prep_binary NaN propagation, then
+// roll_mean(x*y), roll_mean(x), roll_mean(y), roll_sum(notna) (minp 0), roll_var(x),
+// roll_var(y) and  (mxy - mx*my) * (c/(c-1)) / sqrt(vx*vy).
+__global__ void __launch_bounds__(TS_BLOCK)
+k_ts_corr(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ Out,
+          int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W,
+          const uint8_t* __restrict__ present) {
+  extern __shared__ double ring[];  // x [W][64], y [W][64]
+  double* ringy = ring + (int64_t)W * TS_BLOCK;
+  const int lane = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+  if (a >= A) return;
+  const int64_t f = blockIdx.y;
+  const double* x = X + f * D * ld + a;
+  const double* yc = Ycol + f * y_fstride + a;
+  double* o = Out + f * D * ld + a;
+  MeanSt mxy, mx, my;
+  VarSt vx, vy;
+  int64_t i = 0, cnt = 0;
+  int slot = 0;
+  bool first = true;
+  for (int64_t d = 0; d < D; ++d) {
+    bool p = present ? present[d * ld + a] != 0 : true;
+    if (!p) { o[d * ld] = qnan(); continue; }
+    double xr = x[d * ld], yr = yc[d * ld];
+    double xv = xr + 0.0 * yr;
+    double yv = yr + 0.0 * xr;
+    double pv = xv * yv;
+    if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; }
+    if (i >= W) {
+      double ox = ring[slot * TS_BLOCK + lane], oy = ringy[slot * TS_BLOCK + lane];
+      mxy.remove(ox * oy); mx.remove(ox); my.remove(oy); vx.remove(ox); vy.remove(oy);
+      cnt -= (ox + oy == ox + oy);
+    }
+    ring[slot * TS_BLOCK + lane] = xv;
+    ringy[slot * TS_BLOCK + lane] = yv;
+    slot = (slot + 1 == W) ? 0 : slot + 1;
+    mxy.add(pv); mx.add(xv); my.add(yv); vx.add(xv); vy.add(yv);
+    cnt += (xv + yv == xv + yv);
+    double c = (double)cnt;
+    double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (c / (c - 1.0));
+    double den = sqrt(vx.var(W, 1) * vy.var(W, 1));
+    o[d * ld] = num / den;
+    i += 1;
+  }
+}
+
+// ts_regression_fast rolling moments over the pair-valid rows of one column
+// (operations.py:204-240).  `valid` marks rows that survive the reference's dropna()
+// (y and the globally shifted x both non-NaN).  Output NaN elsewhere.
+__global__ void __launch_bounds__(TS_BLOCK)
+k_ts_regression(const double* __restrict__ Yv, const double* __restrict__ Xv,
+                const uint8_t* __restrict__ valid, double* __restrict__ Out, int64_t D, int64_t A,
+                int64_t ld, int W, int rettype) {
+  extern __shared__ double ring[];  // x [W][64], y [W][64]
+  double* ringy = ring + (int64_t)W * TS_BLOCK;
+  const int lane = threadIdx.x;
+  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+  if (a >= A) return;
+  MeanSt mx, my, mxx, mxy, myy;
+  int64_t i = 0;
+  int slot = 0;
+  bool first = true;
+  for (int64_t d = 0; d < D; ++d) {
+    int64_t off = d * ld + a;
+    if (!valid[off]) { Out[off] = qnan(); continue; }
+    double xv = Xv[off], yv = Yv[off];
+    if (first) { mx.init(xv); my.init(yv); mxx.init(xv * xv); mxy.init(xv * yv); myy.init(yv * yv); first = false; }
+    if (i >= W) {
+      double ox = ring[slot * TS_BLOCK + lane], oy = ringy[slot * TS_BLOCK + lane];
+      mx.remove(ox); my.remove(oy); mxx.remove(ox * ox); mxy.remove(ox * oy); myy.remove(oy * oy);
+    }
+    ring[slot * TS_BLOCK + lane] = xv;
+    ringy[slot * TS_BLOCK + lane] = yv;
+    slot = (slot + 1 == W) ? 0 : slot + 1;
+    mx.add(xv); my.add(yv); mxx.add(xv * xv); mxy.add(xv * yv); myy.add(yv * yv);
+    double Mx = mx.result(W), My = my.result(W);
+    double cov = mxy.result(W) - Mx * My;
+    double var_x = mxx.result(W) - Mx * Mx;
+    double beta = cov / var_x;
+    double alpha = My - beta * Mx;
+    double fitted = alpha + beta * xv;
+    double r;
+    switch (rettype) {
+      case 0: r = yv - fitted; break;
+      case 1: r = alpha; break;
+      case 2: r = beta; break;
+      case 3: r = fitted; break;
+      default: {
+        double var_y = myy.result(W) - My * My;
+        r = (cov * cov) / (var_x * var_y);
+      }
+    }
+    Out[off] = r;
+    i += 1;
+  }
+}
+
+static fmx_status launch_ring(const void* kern, dim3 grid, size_t lds, hipStream_t st, void** args) {
+  if (lds > 160 * 1024) {
+    set_error("window too large for the LDS ring (needs " + std::to_string(lds) + " bytes)");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  FMX_HIP(hipLaunchKernel(kern, grid, dim3(TS_BLOCK), args, lds, st));
+  return FMX_OK;
+}
+
+}  // namespace fmx
+
+using namespace fmx;
+
+extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
+                                int64_t ld, int32_t window, const uint8_t* present, void* stream) {
+  FMX_ARG(X && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(op >= FMX_TS_SUM && op <= FMX_TS_BACKFILL, "unknown ts op");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  hipStream_t st = as_stream(stream);
+  int W = window;
+  if (op == FMX_TS_BACKFILL) W = 1;
+  if (op == FMX_TS_DECAY && W < 1) {
+    FMX_HIP(hipMemcpyAsync(Y, X, sizeof(double) * F * D * ld, hipMemcpyDeviceToDevice, st));
+    if (present) {
+      int64_t n = F * D * ld;
+      k_ts_window0<<<(int)std::min<int64_t>(ceil_div(n, 256), 8192), 256, 0, st>>>(X, Y, n, FMX_TS_DELAY, present, D * ld, ld);
+      FMX_LAUNCH_CHECK("k_ts_window0");
+    }
+    return FMX_OK;
+  }
+  if ((op == FMX_TS_DIFF || op == FMX_TS_DELAY) && W == 0) {
+    int64_t n = F * D * ld;
+    k_ts_window0<<<(int)std::min<int64_t>(ceil_div(n, 256), 8192), 256, 0, st>>>(X, Y, n, op, present, D * ld, ld);
+    FMX_LAUNCH_CHECK("k_ts_window0");
+    return FMX_OK;
+  }
+  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&W, (void*)&present};
+  if ((op == FMX_TS_DIFF || op == FMX_TS_DELAY) && W < 0) {
+    int K = -W;
+    size_t lds = (size_t)2 * K * TS_BLOCK * sizeof(double);
+    const void* k = op == FMX_TS_DIFF ? (const void*)k_ts_lead<FMX_TS_DIFF> : (const void*)k_ts_lead<FMX_TS_DELAY>;
+    void* largs[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&K, (void*)&present};
+    return launch_ring(k, grid, lds, st, largs);
+  }
+  FMX_ARG(W >= 1, "window must be >= 1");
+  size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * sizeof(double);
+  const void* k = nullptr;
+  switch (op) {
+    case FMX_TS_SUM: k = (const void*)k_ts<FMX_TS_SUM>; break;
+    case FMX_TS_MEAN: k = (const void*)k_ts<FMX_TS_MEAN>; break;
+    case FMX_TS_STD: k = (const void*)k_ts<FMX_TS_STD>; break;
+    case FMX_TS_VAR: k = (const void*)k_ts<FMX_TS_VAR>; break;
+    case FMX_TS_ZSCORE: k = (const void*)k_ts<FMX_TS_ZSCORE>; break;
+    case FMX_TS_RANK: k = (const void*)k_ts<FMX_TS_RANK>; break;
+    case FMX_TS_DECAY: k = (const void*)k_ts<FMX_TS_DECAY>; break;
+    case FMX_TS_DIFF: k = (const void*)k_ts<FMX_TS_DIFF>; break;
+    case FMX_TS_DELAY: k = (const void*)k_ts<FMX_TS_DELAY>; break;
+    default: k = (const void*)k_ts<FMX_TS_BACKFILL>; break;
+  }
+  return launch_ring(k, grid, lds, st, args);
+}
+
+extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* Out, int64_t F, int64_t D,
+                                  int64_t A, int64_t ld, int64_t y_fstride, int32_t window,
+                                  const uint8_t* present, void* stream) {
+  FMX_ARG(X && Ycol && Out, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(window >= 1, "window must be >= 1");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  int W = window;
+  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
+  size_t lds = (size_t)2 * W * TS_BLOCK * sizeof(double);
+  void* args[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,
+                  (void*)&y_fstride, (void*)&W, (void*)&present};
+  return launch_ring((const void*)k_ts_corr, grid, lds, as_stream(stream), args);
+}
+
+extern "C" fmx_status fmx_ts_regression(const double* Yv, const double* Xv, const uint8_t* valid, double* Out,
+                                        int64_t D, int64_t A, int64_t ld, int32_t window, int32_t rettype,
+                                        void* stream) {
+  FMX_ARG(Yv && Xv && valid && Out, "null panel");
+  FMX_ARG(D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(window >= 1, "window must be >= 1");
+  FMX_ARG(rettype == 0 || rettype == 1 || rettype == 2 || rettype == 3 || rettype == 6, "rettype not implemented");
+  if (D == 0 || A == 0) return FMX_OK;
+  int W = window;
+  int rt = rettype;
+  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), 1);
+  size_t lds = (size_t)2 * W * TS_BLOCK * sizeof(double);
+  void* args[] = {(void*)&Yv, (void*)&Xv, (void*)&valid, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,
+                  (void*)&W, (void*)&rt};
+  return launch_ring((const void*)k_ts_regression, grid, lds, as_stream(stream), args);
+}

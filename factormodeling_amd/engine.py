@@ -1,0 +1,247 @@
+"""Device-tensor API over libfmx: every function takes/returns torch CUDA (HIP) tensors
+laid out ``[F][D][A]`` float64 (asset fastest) and launches the gfx950 kernels on the
+current torch stream.  Shapes are validated on the host before any launch.
+
+This is the layer the drop-in pandas modules, the benchmark and the date-sharded
+multi-GPU driver are built on.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import CS, CSREG, EW, GROUP, RANK, TS, call, ptr, stream_ptr
+
+F64 = torch.float64
+
+
+def _check_panel(X, name="X"):
+    if not isinstance(X, torch.Tensor) or X.device.type != "cuda":
+        raise _lib.FmxError(f"{name} must be a HIP device tensor")
+    if X.dtype != F64:
+        raise _lib.FmxError(f"{name} must be float64")
+    if X.dim() != 3:
+        raise _lib.FmxError(f"{name} must be [F][D][A]")
+    if not X.is_contiguous():
+        raise _lib.FmxError(f"{name} must be contiguous")
+
+
+def _check_present(present, D, A):
+    if present is None:
+        return None
+    if present.dtype != torch.uint8 or tuple(present.shape) != (D, A) or not present.is_contiguous():
+        raise _lib.FmxError("present must be a contiguous uint8 [D][A] device tensor")
+    return present
+
+
+def as3(X):
+    return X if X.dim() == 3 else X.unsqueeze(0)
+
+
+def empty_like(X):
+    return torch.empty_like(X)
+
+
+# ----------------------------------------------------------------------------- time series
+def ts(op: str, X, window: int, present=None, out=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Y = _out(X, out)
+    call("fmx_ts_op", TS[op], ptr(X), ptr(Y), F, D, A, A, int(window), ptr(present), stream_ptr())
+    return Y
+
+
+def ts_corr(X, Ycol, window: int, present=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    if Ycol.dim() == 2:
+        if tuple(Ycol.shape) != (D, A):
+            raise _lib.FmxError("Ycol must be [D][A] or [F][D][A]")
+        ystride = 0
+    else:
+        if tuple(Ycol.shape) != (F, D, A):
+            raise _lib.FmxError("Ycol must be [D][A] or [F][D][A]")
+        ystride = D * A
+    Ycol = Ycol.contiguous()
+    out = torch.empty_like(X)
+    call("fmx_ts_corr", ptr(X), ptr(Ycol), ptr(out), F, D, A, A, ystride, int(window), ptr(present), stream_ptr())
+    return out
+
+
+def ts_regression(Yv, Xv, valid, window: int, rettype: int):
+    D, A = Yv.shape
+    if tuple(Xv.shape) != (D, A) or tuple(valid.shape) != (D, A) or valid.dtype != torch.uint8:
+        raise _lib.FmxError("ts_regression: shape mismatch")
+    out = torch.empty_like(Yv)
+    call("fmx_ts_regression", ptr(Yv), ptr(Xv), ptr(valid), ptr(out), D, A, A, int(window), int(rettype),
+         stream_ptr())
+    return out
+
+
+# ----------------------------------------------------------------------------- cross section
+def _out(X, out):
+    if out is None:
+        return torch.empty_like(X)
+    if out.shape != X.shape or out.dtype != X.dtype or not out.is_contiguous() or out.data_ptr() == X.data_ptr():
+        raise _lib.FmxError("out must be a distinct contiguous tensor shaped like X")
+    return out
+
+
+def cs_moment(op: str, X, present=None, out=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Y = _out(X, out)
+    call("fmx_cs_moment", CS[op], ptr(X), ptr(Y), F, D, A, A, ptr(present), stream_ptr())
+    return Y
+
+
+def cs_rank(X, method="average", present=None, out=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    if method not in RANK:
+        raise ValueError(f"unknown rank method {method!r}")
+    Y = _out(X, out)
+    call("fmx_cs_rank", ptr(X), ptr(Y), F, D, A, A, RANK[method], ptr(present), stream_ptr())
+    return Y
+
+
+def cs_quantile_op(kind: str, X, qlo: float, qhi: float, present=None, out=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Y = _out(X, out)
+    fn = "fmx_cs_winsor" if kind == "winsor" else "fmx_cs_filter_center"
+    call(fn, ptr(X), ptr(Y), F, D, A, A, float(qlo), float(qhi), ptr(present), stream_ptr())
+    return Y
+
+
+def group_op(op: str, X, G, ngroups: int, method="average", present=None):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    if G.dtype != torch.int32 or tuple(G.shape) != (D, A):
+        raise _lib.FmxError("G must be int32 [D][A]")
+    Y = torch.empty_like(X)
+    call("fmx_group_op", GROUP[op], ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method], ptr(present),
+         stream_ptr())
+    return Y
+
+
+def cs_regression(Yv, Xv, rettype: str, present=None):
+    D, A = Yv.shape
+    if tuple(Xv.shape) != (D, A):
+        raise _lib.FmxError("cs_regression: shape mismatch")
+    _check_present(present, D, A)
+    out = torch.empty_like(Yv)
+    call("fmx_cs_regression", ptr(Yv), ptr(Xv), ptr(out), D, A, A, CSREG[rettype], ptr(present), stream_ptr())
+    return out
+
+
+def elementwise(op: str, X, a=0.0, b=0.0):
+    X = X.contiguous()
+    Y = torch.empty_like(X)
+    call("fmx_elementwise", EW[op], ptr(X), ptr(Y), X.numel(), float(a), float(b), stream_ptr())
+    return Y
+
+
+def bucket_codes(X, edges: np.ndarray):
+    X = X.contiguous()
+    e = torch.as_tensor(np.asarray(edges, dtype=np.float64), device=X.device)
+    codes = torch.empty(X.shape, dtype=torch.int32, device=X.device)
+    call("fmx_bucket", ptr(X), ptr(codes), X.numel(), ptr(e), len(edges), stream_ptr())
+    return codes
+
+
+# ----------------------------------------------------------------------------- IC / selection
+def ic_daily(X, R, lags=(1,)):
+    """[n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta) for pairs (X[f][t-L], R[t])."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if tuple(R.shape) != (D, A) or R.dtype != F64 or not R.is_contiguous():
+        raise _lib.FmxError("R must be a contiguous float64 [D][A] device tensor")
+    lag_t = torch.tensor(list(lags), dtype=torch.int32, device=X.device)
+    out = torch.empty((len(lags), 4, F, D), dtype=F64, device=X.device)
+    call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ptr(lag_t), len(lags), ptr(out), stream_ptr())
+    return out
+
+
+def ic_window(daily, d0, d1):
+    """daily [4][F][D]; windows [d0[j], d1[j]) -> [J][F][8]."""
+    _, F, D = daily.shape
+    daily = daily.contiguous()
+    d0t = torch.as_tensor(np.asarray(d0, dtype=np.int32), device=daily.device)
+    d1t = torch.as_tensor(np.asarray(d1, dtype=np.int32), device=daily.device)
+    J = len(d0t)
+    out = torch.empty((J, F, 8), dtype=F64, device=daily.device)
+    call("fmx_ic_window", ptr(daily), F, D, ptr(d0t), ptr(d1t), J, ptr(out), stream_ptr())
+    return out
+
+
+def select_icir_top(metrics, use_rank_icir=True, threshold=0.03, top_x=5):
+    J, F, _ = metrics.shape
+    metrics = metrics.contiguous()
+    order = torch.empty((J, F), dtype=torch.int32, device=metrics.device)
+    w = torch.empty((J, F), dtype=F64, device=metrics.device)
+    call("fmx_select_icir_top", ptr(metrics), J, F, int(bool(use_rank_icir)), float(threshold), int(top_x),
+         ptr(order), ptr(w), stream_ptr())
+    return order, w
+
+
+def zscore_exposures(X):
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    Z = torch.empty_like(X)
+    M = torch.empty_like(X)
+    call("fmx_zscore_exposures", ptr(X), ptr(Z), ptr(M), F, D, A, A, stream_ptr())
+    return Z, M
+
+
+def gram(Z, M=None, d0=0, d1=None):
+    F, D, A = Z.shape
+    d1 = D if d1 is None else d1
+    G = torch.empty((F, F), dtype=F64, device=Z.device)
+    N = torch.empty((F, F), dtype=F64, device=Z.device) if M is not None else None
+    call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, stream_ptr())
+    return G, N
+
+
+def corr_matrix(X, d0=0, d1=None):
+    """Builder-defined factor correlation: C = G / N on fp64 MFMA."""
+    Z, M = zscore_exposures(X)
+    G, N = gram(Z, M, d0, d1)
+    return torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
+
+
+def greedy_prune(C, order, rho=0.7, top_x=None):
+    """Walk ``order``; keep f iff max |C[f, kept]| < rho (host, O(F * kept))."""
+    Cn = C.detach().cpu().numpy() if isinstance(C, torch.Tensor) else np.asarray(C)
+    kept = []
+    for f in order:
+        f = int(f)
+        if kept and np.max(np.abs(Cn[f, kept])) >= rho:
+            continue
+        kept.append(f)
+        if top_x is not None and len(kept) >= top_x:
+            break
+    return kept
+
+
+def device_info():
+    buf = ctypes.create_string_buffer(256)
+    call("fmx_device_info", buf, 256)
+    return buf.value.decode()

@@ -1,0 +1,208 @@
+"""Device-resident factor-panel pipeline (one benchmark "step") and synthetic panels.
+
+Step = the C2 hot path of BASELINE.json on a panel already resident in HBM:
+  1. operator set per factor: ts_mean(20), ts_std(20), ts_zscore(20), ts_rank(10),
+     ts_decay(20), cs_rank, cs_zscore, cs_winsor, market_neutralize
+     (operations.py; each writes its own output panel)
+  2. daily IC / rank-IC / beta at lag 1 (single_factor_metrics) and lag 2
+     (FactorSelector windows) -- one fmx_ic_daily launch
+  3. full-sample metrics + rolling W-window metrics for every processed day
+  4. icir_top selection per day (top_x=5, threshold=-1, factor_selector.py:94-139)
+  5. correlation-based pruning: fp64-MFMA factor Gram + greedy prune (builder-defined)
+
+Multi-GPU: ``ShardedPanel`` holds a rank's date shard plus a halo of the preceding
+dates; ``run_step`` exchanges the halo, runs 1-2 on local dates, all-gathers the daily
+IC series, runs 3-4 redundantly, all-reduces the Gram partials and prunes.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import engine as E
+
+OPS = [("ts", "mean", 20), ("ts", "std", 20), ("ts", "zscore", 20), ("ts", "rank", 10), ("ts", "decay", 20),
+       ("cs_rank", None, None), ("cs", "zscore", None), ("winsor", None, None), ("cs", "market_neutralize", None)]
+MAX_LOOKBACK = 20          # longest rolling window in OPS
+SEL_WINDOW = 60            # FactorSelector window (pipeline.ipynb:355)
+HALO = MAX_LOOKBACK - 1 + 2  # rolling warm-up + IC lag 2
+
+
+@dataclass
+class StepConfig:
+    sel_window: int = SEL_WINDOW
+    top_x: int = 5
+    icir_threshold: float = -1.0
+    prune_rho: float = 0.7
+    ops: list = field(default_factory=lambda: list(OPS))
+
+
+def synthetic_panel(D, A, F, device, seed=0, d_lo=0, d_hi=None, halo=0):
+    """SURVEY 8(d) generator on the device: X ~ N(0,1) with 1% NaN and 5% of values
+    rounded to 1 decimal; R = 0.01 N(0,1) + 0.002 X[d-1,:,0] with 0.5% NaN.  Returns the
+    rows [d_lo - halo, d_hi) of the full panel (identical on every rank: the generator is
+    seeded per date)."""
+    d_hi = D if d_hi is None else d_hi
+    lo = max(0, d_lo - halo)
+    n = d_hi - lo
+    X = torch.empty((F, n, A), dtype=torch.float64, device=device)
+    R = torch.empty((n, A), dtype=torch.float64, device=device)
+    g = torch.Generator(device=device)
+    prev0 = None
+    for k, d in enumerate(range(lo, d_hi)):
+        g.manual_seed(seed * 1_000_003 + d)
+        x = torch.randn((F, A), generator=g, dtype=torch.float64, device=device)
+        u = torch.rand((F, A), generator=g, dtype=torch.float64, device=device)
+        x = torch.where(u < 0.05, torch.round(x * 10) / 10, x)
+        x = torch.where(u > 0.99, torch.full_like(x, float("nan")), x)
+        X[:, k] = x
+        r = 0.01 * torch.randn((A,), generator=g, dtype=torch.float64, device=device)
+        ur = torch.rand((A,), generator=g, dtype=torch.float64, device=device)
+        if d > 0:
+            if prev0 is None:   # first generated row: regenerate date d-1's factor 0
+                g2 = torch.Generator(device=device)
+                g2.manual_seed(seed * 1_000_003 + d - 1)
+                xp = torch.randn((F, A), generator=g2, dtype=torch.float64, device=device)
+                up = torch.rand((F, A), generator=g2, dtype=torch.float64, device=device)
+                xp = torch.where(up < 0.05, torch.round(xp * 10) / 10, xp)
+                xp = torch.where(up > 0.99, torch.full_like(xp, float("nan")), xp)
+                prev0 = xp[0]
+            r = r + 0.002 * torch.nan_to_num(prev0)
+        r = torch.where(ur < 0.005, torch.full_like(r, float("nan")), r)
+        R[k] = r
+        prev0 = x[0]
+    return X, R, lo
+
+
+class ShardedPanel:
+    """A rank's slice of the date axis: owned dates [d_lo, d_hi) plus ``halo`` preceding
+    dates, stored contiguously as X[F][halo + own][A]."""
+
+    def __init__(self, D, A, F, rank, world, device, seed=0, halo=HALO):
+        self.D, self.A, self.F = D, A, F
+        self.rank, self.world = rank, world
+        per = (D + world - 1) // world
+        self.d_lo = min(D, rank * per)
+        self.d_hi = min(D, (rank + 1) * per)
+        self.halo = halo if rank > 0 else 0
+        self.device = device
+        X, R, lo = synthetic_panel(D, A, F, device, seed, self.d_lo, self.d_hi, self.halo)
+        assert lo == self.d_lo - self.halo
+        self.X, self.R = X, R
+        self.own = self.d_hi - self.d_lo
+
+    def exchange_halo(self):
+        """Send my last ``halo`` owned dates to rank+1, receive rank-1's into my halo
+        (RCCL point-to-point over xGMI; gloo on CPU)."""
+        if self.world == 1:
+            return
+        H = HALO
+        reqs = []
+        if self.rank + 1 < self.world:
+            send_x = self.X[:, -H:].contiguous()
+            send_r = self.R[-H:].contiguous()
+            reqs.append(dist.isend(send_x, self.rank + 1))
+            reqs.append(dist.isend(send_r, self.rank + 1))
+        if self.rank > 0:
+            recv_x = torch.empty((self.F, self.halo, self.A), dtype=self.X.dtype, device=self.X.device)
+            recv_r = torch.empty((self.halo, self.A), dtype=self.R.dtype, device=self.R.device)
+            reqs.append(dist.irecv(recv_x, self.rank - 1))
+            reqs.append(dist.irecv(recv_r, self.rank - 1))
+        for r in reqs:
+            r.wait()
+        if self.rank > 0:
+            self.X[:, :self.halo] = recv_x
+            self.R[:self.halo] = recv_r
+
+
+def run_ops(X, cfg: StepConfig, out=None, timers=None):
+    """Operator set over the local panel (halo rows included as warm-up)."""
+    Y = out if out is not None else torch.empty_like(X)
+    for kind, op, w in cfg.ops:
+        t0 = _ev(timers)
+        if kind == "ts":
+            E.ts(op, X, w, None, out=Y)
+        elif kind == "cs_rank":
+            E.cs_rank(X, out=Y)
+        elif kind == "cs":
+            E.cs_moment(op, X, out=Y)
+        elif kind == "winsor":
+            E.cs_quantile_op("winsor", X, 0.01, 0.99, out=Y)
+        _rec(timers, f"{kind}:{op or ''}:{w or ''}", t0)
+    return Y
+
+
+def _ev(timers):
+    if timers is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _rec(timers, name, t0):
+    if timers is None:
+        return
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    timers.append((name, t0, e))
+
+
+def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None):
+    """One pass of the hot path.  Returns (selected weights [J][F] on rank 0's view,
+    kept factor list)."""
+    t0 = _ev(timers)
+    sp.exchange_halo()
+    _rec(timers, "halo", t0)
+    run_ops(sp.X, cfg, timers=timers)
+    # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
+    t0 = _ev(timers)
+    daily = E.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
+    _rec(timers, "ic_daily", t0)
+    t0 = _ev(timers)
+    if sp.world > 1:
+        per = (sp.D + sp.world - 1) // sp.world
+        pad = torch.zeros((2, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
+        pad[..., :daily.shape[3]] = daily
+        parts = [torch.empty_like(pad) for _ in range(sp.world)]
+        dist.all_gather(parts, pad)
+        full = torch.cat(parts, dim=3)[:, :, :, :sp.D].contiguous()
+    else:
+        full = daily.contiguous()
+    _rec(timers, "allgather_ic", t0)
+    t0 = _ev(timers)
+    D = full.shape[3]
+    W = cfg.sel_window
+    proc = list(range(W, D - 1))
+    summ = E.ic_window(full[0].contiguous(), [0], [D])                 # full-sample metrics
+    win = E.ic_window(full[1].contiguous(), [i - W + 1 for i in proc], proc)
+    order, w = E.select_icir_top(win, True, cfg.icir_threshold, cfg.top_x)
+    _rec(timers, "select", t0)
+    # correlation Gram over owned dates, all-reduced
+    t0 = _ev(timers)
+    Xo = sp.X[:, sp.halo:]
+    Z, M = E.zscore_exposures(Xo.contiguous())
+    G, N = E.gram(Z, M)
+    if sp.world > 1:
+        dist.all_reduce(G)
+        dist.all_reduce(N)
+    C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
+    _rec(timers, "gram", t0)
+    t0 = _ev(timers)
+    rir = summ[0, :, 3]
+    full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
+    kept = E.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, cfg.top_x)
+    _rec(timers, "prune", t0)
+    return w, kept
+
+
+def stage_times(timers):
+    torch.cuda.synchronize()
+    out = {}
+    for name, a, b in timers:
+        out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+    return out

@@ -1,0 +1,165 @@
+/*
+ * fmx.h -- C ABI of libfmx, the MI355X (gfx950) engine for the FactorModeling
+ * factor-panel hot path.
+ *
+ * Boundary: the reference (Yuming-Yang/FactorModeling) is pure Python; its "FFI" for this
+ * path is the set of Python functions in operations.py, factor_selector.py,
+ * factor_selection_methods.py and composite_factor.py.  The drop-in modules in
+ * factormodeling_amd/ keep those signatures and bind the entry points below through
+ * ctypes.  Each entry point names the reference function(s) it
+ * replaces.
+ *
+ * Conventions
+ *   - Panels are device pointers to float64 X[F][D][ld] (factor, date, asset; asset
+ *     fastest; ld >= A is the row stride in elements).  Returns R are [D][ld].
+ *   - present: optional device uint8[D][ld]; 0 marks a (date, symbol) pair with no row
+ *     in the reference's long (date, symbol) MultiIndex.  NULL = dense panel.
+ *     Time-series ops walk each symbol's present rows (row-based, as the reference's
+ *     groupby('symbol') + rolling/shift); cross-sectional ops reduce over the present
+ *     rows of a date.  Outputs at absent cells are NaN.
+ *   - stream: a hipStream_t passed as void* (NULL = default stream).  All calls are
+ *     stream-ordered and asynchronous; no call allocates with hipMalloc on the hot
+ *     path except the first use of a row length (pairwise-sum schedules are cached).
+ *   - Errors: every call returns an fmx_status; fmx_last_error() gives a thread-local
+ *     message.  No exceptions cross the ABI.
+ */
+#ifndef FMX_H_
+#define FMX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t fmx_status;
+#define FMX_OK 0
+#define FMX_ERR_ARG 1
+#define FMX_ERR_HIP 2
+#define FMX_ERR_UNSUPPORTED 3
+#define FMX_ERR_NOMEM 4
+
+#define FMX_ABI_VERSION 1
+
+/* time-series ops (fmx_ts_op) */
+#define FMX_TS_SUM 0      /* operations.py:6   ts_sum      rolling(w).sum()            */
+#define FMX_TS_MEAN 1     /* operations.py:10  ts_mean     rolling(w).mean()           */
+#define FMX_TS_STD 2      /* operations.py:14  ts_std      rolling(w).std()            */
+#define FMX_TS_VAR 3      /*                   rolling(w).var() (helper)               */
+#define FMX_TS_ZSCORE 4   /* operations.py:18  ts_zscore                               */
+#define FMX_TS_RANK 5     /* operations.py:23  ts_rank     pct rank of last in window  */
+#define FMX_TS_DECAY 6    /* operations.py:40  ts_decay    linear-weight MA            */
+#define FMX_TS_DIFF 7     /* operations.py:34  ts_diff     diff(w), w may be <= 0      */
+#define FMX_TS_DELAY 8    /* operations.py:37  ts_delay    shift(w), w may be <= 0     */
+#define FMX_TS_BACKFILL 9 /* operations.py:50  ts_backfill ffill()                     */
+
+/* cross-sectional moment ops (fmx_cs_moment) */
+#define FMX_CS_ZSCORE 0            /* operations.py:77  cs_zscore         */
+#define FMX_CS_MEAN 1              /* operations.py:85  cs_mean           */
+#define FMX_CS_MARKET_NEUTRALIZE 2 /* operations.py:171 market_neutralize */
+
+/* rank methods (pandas Series.rank(method=...)) */
+#define FMX_RANK_AVERAGE 0
+#define FMX_RANK_MIN 1
+#define FMX_RANK_MAX 2
+#define FMX_RANK_FIRST 3
+#define FMX_RANK_DENSE 4
+
+/* group ops (fmx_group_op) */
+#define FMX_GROUP_MEAN 0       /* operations.py:112 group_mean            */
+#define FMX_GROUP_NEUTRALIZE 1 /* operations.py:124 group_neutralize      */
+#define FMX_GROUP_NORMALIZE 2  /* operations.py:137 group_normalize       */
+#define FMX_GROUP_RANK 3       /* operations.py:152 group_rank_normalized */
+
+/* elementwise ops (fmx_elementwise) */
+#define FMX_EW_SIGN 0  /* operations.py:88  sign            */
+#define FMX_EW_POWER 1 /* operations.py:91  power(x, a)     */
+#define FMX_EW_LOG 2   /* operations.py:94  log             */
+#define FMX_EW_ABS 3   /* operations.py:97  abs_            */
+#define FMX_EW_CLIP 4  /* operations.py:100 clip(x, a, b)   */
+#define FMX_EW_WHERE 5 /* operations.py:80  cs_bool(cond, a, b), cond as 0/1 */
+
+/* cs_regression rettype (operations.py:248) */
+#define FMX_CSREG_RESID 0
+#define FMX_CSREG_BETA 1
+#define FMX_CSREG_ALPHA 2
+#define FMX_CSREG_FITTED 3
+#define FMX_CSREG_R2 4
+
+/* ---- library ------------------------------------------------------------------ */
+const char* fmx_last_error(void);
+int32_t fmx_abi_version(void);
+/* Writes "gfx950 ... CUs ... HBM bytes" of the current device into buf. */
+fmx_status fmx_device_info(char* buf, int64_t buflen);
+
+/* ---- time series (operations.py:6-51) -------------------------------------------- */
+/* Replaces ts_sum/ts_mean/ts_std/ts_zscore/ts_rank/ts_decay/ts_diff/ts_delay/ts_backfill
+ * (operations.py:6-51).  Y may not alias X.  Rolling sums/means/variances reproduce
+ * pandas' Kahan/Welford kernels bit-for-bit. */
+fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                     int32_t window, const uint8_t* present, void* stream);
+
+/* Builder-defined ts_corr (no reference counterpart): per-symbol rolling Pearson of X[f]
+ * against Ycol (y_fstride = 0: one [D][ld] series shared by all factors, e.g. returns),
+ * pandas Rolling.corr semantics, min_periods = window. */
+fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* Out, int64_t F, int64_t D, int64_t A,
+                       int64_t ld, int64_t y_fstride, int32_t window, const uint8_t* present, void* stream);
+
+/* ts_regression_fast rolling moments (operations.py:185-246) for one [D][ld] pair.
+ * Xv is the globally shifted x; valid marks rows kept by the reference's dropna().
+ * rettype 0 resid, 1 alpha, 2 beta, 3 fitted, 6 R^2.  NaN where not computed. */
+fmx_status fmx_ts_regression(const double* Yv, const double* Xv, const uint8_t* valid, double* Out, int64_t D,
+                             int64_t A, int64_t ld, int32_t window, int32_t rettype, void* stream);
+
+/* ---- cross section (operations.py:54-101, 171-182, 248-304) ---------------------- */
+fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                         const uint8_t* present, void* stream);
+/* cs_rank (operations.py:54-62): (rank - 1) / (rows - 1), rows counting NaN. */
+fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
+                       const uint8_t* present, void* stream);
+/* cs_winsor (operations.py:64-68); qlo/qhi are the fractions numpy sees
+ * (pandas passes q*100 and numpy divides by 100). */
+fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, double qlo,
+                         double qhi, const uint8_t* present, void* stream);
+/* cs_filter_center (operations.py:70-75). */
+fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                double qlo, double qhi, const uint8_t* present, void* stream);
+/* group ops (operations.py:112-168).  G: device int32[D][ld] dense group ids, -1 = NaN. */
+fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F, int64_t D, int64_t A,
+                        int64_t ld, int32_t ngroups, int32_t method, const uint8_t* present, void* stream);
+/* cs_regression (operations.py:248-304) for one [D][ld] pair. */
+fmx_status fmx_cs_regression(const double* Yv, const double* Xv, double* Out, int64_t D, int64_t A, int64_t ld,
+                             int32_t rettype, const uint8_t* present, void* stream);
+/* elementwise over n contiguous doubles (operations.py:80-101). */
+fmx_status fmx_elementwise(int32_t op, const double* X, double* Y, int64_t n, double a, double b, void* stream);
+/* bucket (operations.py:104-110): pd.cut(right=True, include_lowest=True) label codes. */
+fmx_status fmx_bucket(const double* X, int32_t* codes, int64_t n, const double* edges, int32_t n_edges,
+                      void* stream);
+
+/* ---- IC, metrics, selection (factor_selector.py:26-139, factor_selection_methods.py:6-26) */
+/* Daily stats for each lag in lags_dev[0..n_lags) (device int32): pairs (X[f][t-L], R[t]).
+ * out: [n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta); NaN where undefined. */
+fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
+                        const int32_t* lags_dev, int32_t n_lags, double* out, void* stream);
+/* Window summaries of one lag's daily stats [4][F][D] over J date windows [d0, d1).
+ * out: [J][F][8] = IC, IC_IR, rank_IC, rank_IC_IR, tstat, n_beta, pct_pos, n_days. */
+fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev, const int32_t* d1_dev,
+                         int64_t J, double* out, void* stream);
+/* icir_top_selector (factor_selection_methods.py:6-26) for J days of window metrics.
+ * order_out [J][F] (rank_IC_IR-descending factor order), w_out [J][F] weights. */
+fmx_status fmx_select_icir_top(const double* metrics, int64_t J, int64_t F, int32_t use_rank_icir,
+                               double threshold, int32_t top_x, int32_t* order_out, double* w_out, void* stream);
+
+/* ---- factor correlation GEMM (builder-defined) ------------------------ */
+/* Z, M: per-date z-scored exposures and validity (0/1) as float64 [F][D][ld]. */
+fmx_status fmx_zscore_exposures(const double* X, double* Z, double* M, int64_t F, int64_t D, int64_t A,
+                                int64_t ld, void* stream);
+/* G[F][F] += sum_{d in [d0,d1), a} Z[i][d][a] Z[j][d][a] and N[F][F] likewise for M,
+ * on fp64 MFMA (v_mfma_f64_16x16x4_f64).  accumulate = 0 overwrites. */
+fmx_status fmx_gram(const double* Z, const double* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
+                    int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMX_H_ */

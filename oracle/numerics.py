@@ -23,6 +23,7 @@ from __future__ import annotations
 import numpy as np
 
 PW_BLOCKSIZE = 128
+BUFSIZE = 8192
 
 
 # --------------------------------------------------------------------------- pairwise sum
@@ -30,7 +31,12 @@ def pairwise_sum(a: np.ndarray) -> np.ndarray:
     """numpy float64 ``a.sum(axis=-1)`` bit-for-bit, vectorised over leading axes."""
     a = np.asarray(a, dtype=np.float64)
     n = a.shape[-1]
-    return 0.0 + _pw(a, 0, n)
+    # the ufunc reduction iterates in buffer-sized chunks (8192 elements) and adds the
+    # chunks' pairwise sums sequentially
+    res = 0.0 + _pw(a, 0, min(n, BUFSIZE))
+    for lo in range(BUFSIZE, n, BUFSIZE):
+        res = res + _pw(a, lo, min(BUFSIZE, n - lo))
+    return res
 
 
 def _pw(a, lo, n):

@@ -155,30 +155,34 @@ def ts_backfill(x, present=None):
 
 
 def ts_corr(x, y, window, present=None):
-    """Builder-defined (no reference counterpart; parity unpinned): per-symbol rolling
-    Pearson correlation, min_periods=window, pandas ``Rolling.corr`` formula
-    cov(x,y) / (std(x) * std(y)) on pair-valid rows (both non-NaN)."""
+    """Builder-defined (no reference counterpart; pinned to pandas, not the reference):
+    per-symbol ``x.rolling(window).corr(y)``.  pandas ``Rolling.corr`` = prep_binary NaN
+    propagation, then (mean(xy) - mean(x) mean(y)) * (c / (c - 1)) / sqrt(var(x) var(y))
+    with roll_mean / roll_sum(notna, minp=0) / roll_var (ddof=1)."""
+    def f(cx, cy):
+        with np.errstate(all="ignore"):
+            xv = cx + 0 * cy
+            yv = cy + 0 * cx
+            mxy = nm.roll_mean(xv * yv, window)
+            mx = nm.roll_mean(xv, window)
+            my = nm.roll_mean(yv, window)
+            # roll_sum with min_periods=0: windows are never NaN
+            cnt = _roll_count(~np.isnan(xv + yv), window)
+            vx = nm.roll_var(xv, window, 1)
+            vy = nm.roll_var(yv, window, 1)
+            num = (mxy - mx * my) * (cnt / (cnt - 1))
+            den = (vx * vy) ** 0.5
+            return num / den
     xc, rows = _compact(np.asarray(x, dtype=np.float64), present)
     yc, _ = _compact(np.asarray(y, dtype=np.float64), present)
-    T, A = xc.shape
-    out = np.full(xc.shape, np.nan)
-    for i in range(window - 1, T):
-        wx = xc[i - window + 1:i + 1]
-        wy = yc[i - window + 1:i + 1]
-        ok = ~(np.isnan(wx) | np.isnan(wy))
-        n = ok.sum(axis=0)
-        full = n >= window
-        with np.errstate(all="ignore"):
-            mx = np.where(ok, wx, 0).sum(0) / n
-            my = np.where(ok, wy, 0).sum(0) / n
-            dx = np.where(ok, wx - mx, 0)
-            dy = np.where(ok, wy - my, 0)
-            sxy = (dx * dy).sum(0)
-            sxx = (dx * dx).sum(0)
-            syy = (dy * dy).sum(0)
-            r = sxy / np.sqrt(sxx * syy)
-        out[i] = np.where(full, r, np.nan)
-    return _expand(out, rows, x.shape)
+    return _expand(f(xc, yc), rows, x.shape)
+
+
+def _roll_count(ok, window):
+    c = np.cumsum(ok.astype(np.int64), axis=0)
+    out = c.copy()
+    out[window:] = c[window:] - c[:-window]
+    return out.astype(np.float64)
 
 
 # --------------------------------------------------------------------------- cross section

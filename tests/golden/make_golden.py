@@ -70,6 +70,8 @@ def put_series(store, key, ser: pd.Series, dates, syms):
     store[key + "__d"] = d
     store[key + "__s"] = s
     store[key + "__v"] = ser.to_numpy(dtype=np.float64, na_value=np.nan)
+    store[key + "__name"] = np.array("" if ser.name is None else str(ser.name))
+    store[key + "__hasname"] = np.array(ser.name is not None)
 
 
 # --------------------------------------------------------------------------- panels
@@ -278,8 +280,24 @@ def gen_composite(ref_cf, rng):
     return st, cases
 
 
+def gen_ts_corr(rng):
+    """Builder-defined ts_corr pinned to pandas (third-party), not to the reference:
+    per symbol ``x.rolling(w).corr(y)``."""
+    dates, syms, x, y, g = ops_panel(rng)
+    st = {"dates": np.array([str(d.date()) for d in dates]), "syms": np.array(syms)}
+    put_series(st, "in_x", x, dates, syms)
+    put_series(st, "in_y", y, dates, syms)
+    for w in (3, 5, 20):
+        parts = [xs.rolling(w).corr(y.xs(sym, level="symbol", drop_level=False))
+                 for sym, xs in x.groupby(level="symbol")]
+        out = pd.concat(parts).reindex(x.index)
+        put_series(st, f"out_ts_corr_{w}", out, dates, syms)
+    return st
+
+
 def main():
     warnings.filterwarnings("ignore")
+    os.environ["TQDM_DISABLE"] = "1"
     ref_ops, ref_fs, ref_fsm, ref_cf = import_reference()
     import scipy
     manifest = {
@@ -304,6 +322,10 @@ def main():
     st, cases = gen_composite(ref_cf, np.random.default_rng(400))
     np.savez_compressed(os.path.join(OUT, "composite.npz"), **st)
     manifest["files"]["composite.npz"] = {"seed": 400, "D": 40, "A": 30, "F": 12, "cases": cases}
+    st = gen_ts_corr(np.random.default_rng(500))
+    np.savez_compressed(os.path.join(OUT, "ts_corr_pandas.npz"), **st)
+    manifest["files"]["ts_corr_pandas.npz"] = {"seed": 500, "D": 60, "A": 40,
+                                               "pinned_to": "pandas Rolling.corr (no reference counterpart)"}
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print("wrote", sorted(manifest["files"]))

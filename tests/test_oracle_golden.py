@@ -106,3 +106,14 @@ def test_composite_vs_reference():
     for meth in ("zscore", "rank"):
         out = OC.weighted_composite_factor(X, names, sd, st["sel_W"], meth)
         assert_close(out.ravel(), st[f"out_wcf_{meth}"], rtol=1e-9, atol=1e-12, what=f"wcf_{meth}")
+
+
+def test_ts_corr_vs_pandas():
+    """ts_corr has no reference counterpart; it is pinned to pandas Rolling.corr."""
+    st = load("ts_corr_pandas.npz")
+    D, A = len(st["dates"]), len(st["syms"])
+    x, _ = dense(st, "in_x", D, A)
+    y, _ = dense(st, "in_y", D, A)
+    for w in (3, 5, 20):
+        out = O.ts_corr(x, y, w)
+        assert_close(gather(out, st, f"out_ts_corr_{w}"), st[f"out_ts_corr_{w}__v"], exact=True, what=f"ts_corr_{w}")
