@@ -40,13 +40,19 @@ SIGNATURES = {
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
+    "fmx_comp_adj": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
+    "fmx_comp_proxy": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
+    "fmx_comp_combine": [c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp],
+    "fmx_wcomp_pct": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "fmx_wcomp_proxy": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
+    "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"fmx_last_error": c_cp}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)
 CS = dict(zscore=0, mean=1, market_neutralize=2)
-RANK = dict(average=0, min=1, max=2, first=3, dense=4)
+RANK = dict(average=0, min=1, max=2, first=3, dense=4, scipy_average=5)
 GROUP = dict(mean=0, neutralize=1, normalize=2, rank=3)
 EW = dict(sign=0, power=1, log=2, abs=3, clip=4, where=5)
 CSREG = dict(resid=0, beta=1, alpha=2, fitted=3, r2=4)

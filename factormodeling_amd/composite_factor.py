@@ -1,0 +1,174 @@
+"""Drop-in replacement for the reference's ``composite_factor.py``.
+
+``composite_factor_calculation`` (composite_factor.py:137-218) and
+``weighted_composite_factor`` (:220-342) keep their signatures and outputs (Series named
+``composite_factor`` on ``factors_df.index``); the per-date percentiles, suffix scaling,
+prefix-group proxies, z-score / rank normalisation, weighting and demeaning run in the
+gfx950 kernels of ``csrc/composite.hip`` and ``csrc/cs_ops.hip``.  The two plotting helpers
+the notebook imports (pipeline.ipynb:55) are host-side matplotlib code, as in the
+reference.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+from . import engine
+from .panel import device, panel_index
+
+
+def _prefix_groups(names):
+    groups = {}
+    for k, n in enumerate(names):
+        groups.setdefault(n.split("_", 1)[0], []).append(k)
+    return groups
+
+
+def composite_factor_calculation(factors_df: pd.DataFrame, selected_factors: list, method: str = "zscore"):
+    """composite_factor.py:137-218"""
+    if method not in ("zscore", "rank"):
+        raise ValueError("method must be 'zscore' or 'rank'")
+    pos = list(selected_factors)
+    P = panel_index(factors_df.index)
+    dev = device()
+    X = P.to_device(factors_df[pos].to_numpy(dtype=np.float64, na_value=np.nan), dev)
+    pres = P.present(dev)
+    Adj = engine.comp_adj(X, list(range(len(pos))), [engine.suffix_code(n) for n in pos])
+    if pres is not None:
+        Adj.masked_fill_(pres.unsqueeze(0) == 0, float("nan"))
+    groups = list(_prefix_groups(pos).values())
+    Prox = engine.comp_proxy(Adj, groups)
+    if method == "zscore":
+        Nrm = engine.cs_moment("market_neutralize", Prox, pres)   # safe_zcol == market_neutralize
+        comp = engine.comp_combine(Nrm, 0, pres)
+    else:
+        Nrm = engine.cs_rank(Prox, "scipy_average", pres)
+        comp = engine.comp_combine(Nrm, 1, pres)
+    vals = P.from_device(comp.unsqueeze(0))[:, 0]
+    return pd.Series(vals, index=factors_df.index, name="composite_factor")
+
+
+def _weighted_plan(P, selection_df: pd.DataFrame, used: list):
+    """Per selection row: selected columns (selection_df column order), suffix codes,
+    prefix groups, group weights and pooled suffix column lists."""
+    col_of = {c: k for k, c in enumerate(used)}
+    rows = []
+    for date, weights in selection_df.iterrows():
+        today = weights[weights > 0].index.tolist()
+        d = P.dates.get_indexer([date])[0] if len(P.dates) else -1
+        if not today or d < 0:
+            rows.append((-1, [], [], [], []))
+            continue
+        groups = _prefix_groups(today)
+        gidx = {}
+        for g, (p, facs) in enumerate(groups.items()):
+            for k in facs:
+                gidx[k] = g
+        gw = [weights[[today[k] for k in facs]].sum() for facs in groups.values()]
+        gws = sum(gw)
+        gw = [x / gws for x in gw] if gws > 0 else [1 / len(gw)] * len(gw)
+        rows.append((int(d), [col_of[c] for c in today], [engine.suffix_code(c) for c in today],
+                     [gidx[k] for k in range(len(today))], gw))
+    J = len(rows)
+    KMAX = max([1] + [len(r[1]) for r in rows])
+    col = np.zeros((J, KMAX), np.int32)
+    suf = np.zeros((J, KMAX), np.int32)
+    grp = np.full((J, KMAX), -1, np.int32)
+    gwa = np.zeros((J, KMAX), np.float64)
+    ncol = np.zeros(J, np.int32)
+    ngrp = np.zeros(J, np.int32)
+    pdate = np.full(J, -1, np.int32)
+    soff = [0]
+    scol = []
+    for j, (d, cs, ss, gs, gw) in enumerate(rows):
+        pdate[j] = d
+        ncol[j] = len(cs)
+        ngrp[j] = len(gw)
+        col[j, :len(cs)] = cs
+        suf[j, :len(ss)] = ss
+        grp[j, :len(gs)] = gs
+        gwa[j, :len(gw)] = gw
+        for s in range(1, 5):
+            scol.extend(c for c, sc in zip(cs, ss) if sc == s)
+            soff.append(len(scol))
+    return {"pdate": pdate, "ncol": ncol, "col": col, "suf": suf, "grp": grp, "ngrp": ngrp, "gw": gwa,
+            "KMAX": KMAX, "soff": np.asarray(soff, np.int32), "scol": np.asarray(scol or [0], np.int32)}
+
+
+def weighted_composite_factor(factors_df: pd.DataFrame, selection_df: pd.DataFrame, method: str = "zscore") -> pd.Series:
+    """composite_factor.py:220-342"""
+    if method not in ("zscore", "rank"):
+        raise ValueError("method must be 'zscore' or 'rank'")
+    if len(selection_df) == 0:
+        raise ValueError("No objects to concatenate")
+    used = [c for c in selection_df.columns if (selection_df[c] > 0).any()]
+    P = panel_index(factors_df.index)
+    dev = device()
+    X = P.to_device(factors_df[used].to_numpy(dtype=np.float64, na_value=np.nan), dev) if used else \
+        torch.zeros((1, P.D, P.A), dtype=torch.float64, device=dev)
+    plan = _weighted_plan(P, selection_df, used)
+    out = engine.wcomp(X, plan, method, P.present(dev))
+    vals = P.from_device(out.unsqueeze(0))[:, 0]
+    return pd.Series(vals, index=factors_df.index, name="composite_factor")
+
+
+# ----------------------------------------------------------------------------- plotting (host)
+def plot_factor_distributions(factors_df: pd.DataFrame, exclude: list = None, bins: int = 50, ncols: int = 3,
+                              figsize: tuple = (15, 5)):
+    """composite_factor.py:17-44 -- histogram grid of factor columns (host matplotlib)."""
+    import matplotlib.pyplot as plt
+    exclude = exclude or []
+    cols = [c for c in factors_df.columns if c not in exclude]
+    nrows = max(1, math.ceil(len(cols) / ncols))
+    fig, axes = plt.subplots(nrows, ncols, figsize=(figsize[0], figsize[1] * nrows), squeeze=False)
+    flat = axes.ravel()
+    for ax, c in zip(flat, cols):
+        ax.hist(factors_df[c].dropna(), bins=bins, density=True, alpha=0.7)
+        ax.set_title(c)
+        ax.set_xlabel("Value")
+        ax.set_ylabel("Density")
+    for ax in flat[len(cols):]:
+        ax.axis("off")
+    plt.tight_layout()
+    plt.show()
+
+
+def plot_quantile_backtests_log(com_factors_df: pd.DataFrame, returns: pd.Series, n_groups: int = 5, ncols: int = 2,
+                                figsize: tuple = (20, 6)):
+    """composite_factor.py:47-134 -- per-date quantile buckets (1 = top), lagged one row
+    per symbol, mean log return per bucket, cumulative P&L and the L1-S{n} spread."""
+    import matplotlib.pyplot as plt
+
+    def buckets(feature: pd.Series) -> pd.DataFrame:
+        lbl = feature.groupby(level="date").transform(
+            lambda x: pd.qcut(x.rank(method="first"), n_groups, labels=False, duplicates="drop"))
+        q = (n_groups - lbl).astype("Int64").groupby(level="symbol").shift(1)
+        df = pd.DataFrame({"log_ret": returns, "group": q}).dropna(subset=["group", "log_ret"])
+        g = df.reset_index().groupby(["date", "group"])["log_ret"].mean().unstack(level="group").sort_index()
+        return g.reindex(columns=range(1, n_groups + 1))
+
+    facs = list(com_factors_df.columns)
+    nrows = max(1, math.ceil(len(facs) / ncols))
+    fig, axes = plt.subplots(nrows, ncols, figsize=(figsize[0], figsize[1] * nrows), squeeze=False)
+    for i, fac in enumerate(facs):
+        ax = axes[i // ncols][i % ncols]
+        g = buckets(com_factors_df[fac])
+        cum = np.expm1(g.cumsum())
+        cum[f"DN_L1-S{n_groups}"] = np.expm1((g[1] - g[n_groups]).cumsum())
+        for line in cum.columns:
+            if str(line).startswith("DN_L1-S"):
+                ax.plot(cum.index, cum[line], label=line, color="black", linewidth=2)
+            else:
+                ax.plot(cum.index, cum[line], label=line)
+        ax.set_title(fac)
+        ax.set_xlabel("Date")
+        ax.set_ylabel("Cumulative Return")
+        ax.legend(loc="upper left", fontsize="small")
+        ax.grid(True)
+    for k in range(len(facs), nrows * ncols):
+        fig.delaxes(axes[k // ncols][k % ncols])
+    plt.tight_layout()
+    plt.show()

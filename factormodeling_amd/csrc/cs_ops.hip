@@ -125,11 +125,17 @@ k_cs_rank(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64
   int nrow, nv;
   block_exscan<CS_NT>(nrow_l, iscr, &nrow);
   block_exscan<CS_NT>(nv_l, iscr, &nv);
+  if (method == FMX_RANK_AVERAGE_PROPAGATE && nv < nrow) {
+    // scipy.stats.rankdata(nan_policy='propagate'): one NaN makes the whole row NaN
+    for (int64_t a = threadIdx.x; a < A; a += CS_NT) y[a] = qnan();
+    return;
+  }
+  const bool single_half = (method != FMX_RANK_AVERAGE_PROPAGATE) && nrow == 1;
   // NaN / absent rows are written here (sorted members are written below)
   for (int64_t a = threadIdx.x; a < A; a += CS_NT) {
     bool p = prow ? prow[a] != 0 : true;
     if (!p) y[a] = qnan();
-    else if (!(x[a] == x[a])) y[a] = (nrow == 1) ? 0.5 : qnan();
+    else if (!(x[a] == x[a])) y[a] = single_half ? 0.5 : qnan();
   }
   bitonic_sort<CS_NT>(keys, idx, P);
   // dense ranks need the number of distinct keys before each position
@@ -149,7 +155,7 @@ k_cs_rank(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64
       base += (p == 0 || keys[p] != keys[p - 1]);
       double r = (double)base;
       int a = idx[p];
-      y[a] = (nrow == 1) ? 0.5 : (r - 1.0) / (double)(nrow - 1);
+      y[a] = single_half ? 0.5 : (r - 1.0) / (double)(nrow - 1);
     }
     return;
   }
@@ -166,7 +172,7 @@ k_cs_rank(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64
       default: r = (double)less + (double)(eq + 1) / 2.0;
     }
     int a = idx[p];
-    y[a] = (nrow == 1) ? 0.5 : (r - 1.0) / (double)(nrow - 1);
+    y[a] = single_half ? 0.5 : (r - 1.0) / (double)(nrow - 1);
   }
 }
 
@@ -475,7 +481,7 @@ extern "C" fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t
                                   int32_t method, const uint8_t* present, void* stream) {
   FMX_ARG(X && Y, "null panel");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
-  FMX_ARG(method >= FMX_RANK_AVERAGE && method <= FMX_RANK_DENSE, "unknown rank method");
+  FMX_ARG(method >= FMX_RANK_AVERAGE && method <= FMX_RANK_AVERAGE_PROPAGATE, "unknown rank method");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   int P = next_pow2((int)A);
   if (P < 2) P = 2;

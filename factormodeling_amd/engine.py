@@ -245,3 +245,97 @@ def device_info():
     buf = ctypes.create_string_buffer(256)
     call("fmx_device_info", buf, 256)
     return buf.value.decode()
+
+
+# ----------------------------------------------------------------------------- composites
+SUFFIXES = ["_eq", "_flx", "_long", "_short"]          # codes 1..4 (composite_factor.py:158-163)
+_QLO = np.array([0, 10, 2, 2, 2], dtype=np.float64)
+_QHI = np.array([0, 90, 98, 98, 98], dtype=np.float64)
+
+
+def suffix_code(name: str) -> int:
+    """composite_factor.py applies the suffix rules in this order; first match wins."""
+    for k, s in enumerate(SUFFIXES):
+        if name.endswith(s):
+            return k + 1
+    return 0
+
+
+def _qfrac(dev):
+    # np.nanpercentile(clean, [q_low, q_high]) divides integer percents by 100
+    lo = torch.as_tensor(np.true_divide(_QLO, 100), device=dev)
+    hi = torch.as_tensor(np.true_divide(_QHI, 100), device=dev)
+    return lo, hi
+
+
+def _i32(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(a, dtype=np.int32)), device=dev)
+
+
+def comp_adj(X, cols, suffix_codes):
+    _check_panel(X)
+    F, D, A = X.shape
+    K = len(cols)
+    dev = X.device
+    lo, hi = _qfrac(dev)
+    c, s = _i32(cols, dev), _i32(suffix_codes, dev)
+    Adj = torch.empty((K, D, A), dtype=F64, device=dev)
+    call("fmx_comp_adj", ptr(X), ptr(c), ptr(s), ptr(lo), ptr(hi), ptr(Adj), K, D, A, stream_ptr())
+    return Adj
+
+
+def comp_proxy(Adj, groups):
+    """groups: list of column-index lists into Adj."""
+    K, D, A = Adj.shape
+    dev = Adj.device
+    gcols = _i32([c for g in groups for c in g], dev)
+    goff = _i32(np.concatenate([[0], np.cumsum([len(g) for g in groups])]), dev)
+    G = len(groups)
+    P = torch.empty((G, D, A), dtype=F64, device=dev)
+    call("fmx_comp_proxy", ptr(Adj), ptr(gcols), ptr(goff), ptr(P), G, D, A, stream_ptr())
+    return P
+
+
+def comp_combine(Nrm, mode, present=None):
+    G, D, A = Nrm.shape
+    out = torch.empty((D, A), dtype=F64, device=Nrm.device)
+    call("fmx_comp_combine", ptr(Nrm), G, D, A, int(mode), ptr(present), ptr(out), stream_ptr())
+    return out
+
+
+def wcomp(X, plan, method, present=None):
+    """weighted_composite_factor device stages for a host-built ``plan`` (see
+    composite_factor._weighted_plan).  Returns the [D][A] composite (0 where unselected)."""
+    _check_panel(X)
+    F, D, A = X.shape
+    dev = X.device
+    J = len(plan["pdate"])
+    out = torch.zeros((D, A), dtype=F64, device=dev)
+    if J == 0:
+        return out
+    KMAX = plan["KMAX"]
+    pdate, ncol = _i32(plan["pdate"], dev), _i32(plan["ncol"], dev)
+    col, suf, grp = _i32(plan["col"], dev), _i32(plan["suf"], dev), _i32(plan["grp"], dev)
+    soff, scol = _i32(plan["soff"], dev), _i32(plan["scol"], dev)
+    ngrp = _i32(plan["ngrp"], dev)
+    gw = torch.as_tensor(plan["gw"], device=dev)
+    lo, hi = _qfrac(dev)
+    lohi = torch.empty((J, 4, 3), dtype=F64, device=dev)
+    call("fmx_wcomp_pct", ptr(X), ptr(pdate), ptr(soff), ptr(scol), J, D, A, ptr(lo), ptr(hi), ptr(lohi),
+         stream_ptr())
+    G = max(1, int(plan["ngrp"].max()))
+    P = torch.empty((G, J, A), dtype=F64, device=dev)
+    call("fmx_wcomp_proxy", ptr(X), ptr(pdate), ptr(ncol), ptr(col), ptr(suf), ptr(grp), KMAX, J, D, A, ptr(lohi), G,
+         ptr(P), stream_ptr())
+    presJ = None
+    if present is not None:
+        pd_idx = torch.as_tensor(np.maximum(plan["pdate"], 0), device=dev, dtype=torch.long)
+        presJ = present[pd_idx].contiguous()
+        P.masked_fill_(presJ.unsqueeze(0) == 0, float("nan"))
+    if method == "zscore":
+        Nrm = cs_moment("market_neutralize", P, presJ)
+    else:
+        Nrm = cs_rank(P, "scipy_average", presJ)
+    call("fmx_wcomp_combine", ptr(Nrm), ptr(pdate), ptr(ngrp), ptr(gw), KMAX, J, D, A, ptr(present), ptr(out),
+         stream_ptr())
+    return out

@@ -16,7 +16,6 @@ IC series, runs 3-4 redundantly, all-reduces the Gram partials and prunes.
 """
 from __future__ import annotations
 
-import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -119,25 +118,43 @@ class ShardedPanel:
             self.R[:self.halo] = recv_r
 
 
-def run_ops(X, cfg: StepConfig, out=None, timers=None):
+class EngineBackend:
+    """The product compute backend: libfmx kernels on the local GPU."""
+
+    def op(self, kind, op, w, X, out):
+        if kind == "ts":
+            return E.ts(op, X, w, None, out=out)
+        if kind == "cs_rank":
+            return E.cs_rank(X, out=out)
+        if kind == "cs":
+            return E.cs_moment(op, X, out=out)
+        if kind == "winsor":
+            return E.cs_quantile_op("winsor", X, 0.01, 0.99, out=out)
+        raise ValueError(kind)
+
+    ic_daily = staticmethod(E.ic_daily)
+    ic_window = staticmethod(E.ic_window)
+    select_icir_top = staticmethod(E.select_icir_top)
+    zscore_exposures = staticmethod(E.zscore_exposures)
+    gram = staticmethod(E.gram)
+    greedy_prune = staticmethod(E.greedy_prune)
+
+
+ENGINE = EngineBackend()
+
+
+def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE):
     """Operator set over the local panel (halo rows included as warm-up)."""
     Y = out if out is not None else torch.empty_like(X)
     for kind, op, w in cfg.ops:
         t0 = _ev(timers)
-        if kind == "ts":
-            E.ts(op, X, w, None, out=Y)
-        elif kind == "cs_rank":
-            E.cs_rank(X, out=Y)
-        elif kind == "cs":
-            E.cs_moment(op, X, out=Y)
-        elif kind == "winsor":
-            E.cs_quantile_op("winsor", X, 0.01, 0.99, out=Y)
+        be.op(kind, op, w, X, Y)
         _rec(timers, f"{kind}:{op or ''}:{w or ''}", t0)
     return Y
 
 
 def _ev(timers):
-    if timers is None:
+    if timers is None or not torch.cuda.is_available():
         return None
     e = torch.cuda.Event(enable_timing=True)
     e.record()
@@ -145,23 +162,23 @@ def _ev(timers):
 
 
 def _rec(timers, name, t0):
-    if timers is None:
+    if timers is None or t0 is None:
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     timers.append((name, t0, e))
 
 
-def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None):
-    """One pass of the hot path.  Returns (selected weights [J][F] on rank 0's view,
-    kept factor list)."""
+def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE):
+    """One pass of the hot path.  Returns (selected weights [J][F] (every rank holds the
+    full result), kept factor list)."""
     t0 = _ev(timers)
     sp.exchange_halo()
     _rec(timers, "halo", t0)
-    run_ops(sp.X, cfg, timers=timers)
+    run_ops(sp.X, cfg, timers=timers, be=be)
     # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
-    daily = E.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
+    daily = be.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
     _rec(timers, "ic_daily", t0)
     t0 = _ev(timers)
     if sp.world > 1:
@@ -178,15 +195,15 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None):
     D = full.shape[3]
     W = cfg.sel_window
     proc = list(range(W, D - 1))
-    summ = E.ic_window(full[0].contiguous(), [0], [D])                 # full-sample metrics
-    win = E.ic_window(full[1].contiguous(), [i - W + 1 for i in proc], proc)
-    order, w = E.select_icir_top(win, True, cfg.icir_threshold, cfg.top_x)
+    summ = be.ic_window(full[0].contiguous(), [0], [D])                # full-sample metrics
+    win = be.ic_window(full[1].contiguous(), [i - W + 1 for i in proc], proc)
+    order, w = be.select_icir_top(win, True, cfg.icir_threshold, cfg.top_x)
     _rec(timers, "select", t0)
     # correlation Gram over owned dates, all-reduced
     t0 = _ev(timers)
     Xo = sp.X[:, sp.halo:]
-    Z, M = E.zscore_exposures(Xo.contiguous())
-    G, N = E.gram(Z, M)
+    Z, M = be.zscore_exposures(Xo.contiguous())
+    G, N = be.gram(Z, M)
     if sp.world > 1:
         dist.all_reduce(G)
         dist.all_reduce(N)
@@ -195,9 +212,13 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None):
     t0 = _ev(timers)
     rir = summ[0, :, 3]
     full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
-    kept = E.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, cfg.top_x)
+    kept = be.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, cfg.top_x)
     _rec(timers, "prune", t0)
     return w, kept
+
+
+def _ev_ok():
+    return torch.cuda.is_available()
 
 
 def stage_times(timers):

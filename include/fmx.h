@@ -64,6 +64,7 @@ typedef int32_t fmx_status;
 #define FMX_RANK_MAX 2
 #define FMX_RANK_FIRST 3
 #define FMX_RANK_DENSE 4
+#define FMX_RANK_AVERAGE_PROPAGATE 5 /* scipy.stats.rankdata: any NaN -> row NaN; no 0.5 rule */
 
 /* group ops (fmx_group_op) */
 #define FMX_GROUP_MEAN 0       /* operations.py:112 group_mean            */
@@ -158,6 +159,33 @@ fmx_status fmx_zscore_exposures(const double* X, double* Z, double* M, int64_t F
  * on fp64 MFMA (v_mfma_f64_16x16x4_f64).  accumulate = 0 overwrites. */
 fmx_status fmx_gram(const double* Z, const double* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
                     int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
+
+/* ---- composite factors (composite_factor.py:137-342) ------------------------------- */
+/* composite_factor_calculation preprocessing (:157-178): Adj[k] = suffix-scaled X[cols[k]]
+ * with per-(column, date) numpy linear nanpercentiles.  suffix codes 0 none, 1 _eq,
+ * 2 _flx, 3 _long, 4 _short; qlo/qhi: device double[5] percentile fractions per code. */
+fmx_status fmx_comp_adj(const double* X, const int32_t* cols_dev, const int32_t* suffix_dev, const double* qlo_dev,
+                        const double* qhi_dev, double* Adj, int64_t K, int64_t D, int64_t A, void* stream);
+/* prefix-group proxies (:181-190): skipna mean over the columns gcols[goff[g]..goff[g+1]). */
+fmx_status fmx_comp_proxy(const double* Adj, const int32_t* gcols_dev, const int32_t* goff_dev, double* Prox,
+                          int64_t G, int64_t D, int64_t A, void* stream);
+/* combine normalised proxies (mode 0 skipna mean / 1 skipna sum) and demean (:204-216). */
+fmx_status fmx_comp_combine(const double* Nrm, int64_t G, int64_t D, int64_t A, int32_t mode,
+                            const uint8_t* present, double* Out, void* stream);
+/* weighted_composite_factor (:220-342): pooled suffix percentiles per selection row j
+ * (columns scol[soff[4j+s-1] .. soff[4j+s]) for suffix s=1..4); lohi[J][4][3] = lo, hi, n. */
+fmx_status fmx_wcomp_pct(const double* X, const int32_t* pdate, const int32_t* soff, const int32_t* scol, int64_t J,
+                         int64_t D, int64_t A, const double* qlo_dev, const double* qhi_dev, double* lohi,
+                         void* stream);
+/* per-row prefix-group proxies Prox[G][J][A] from the row plan (ncol, col, suf, grp). */
+fmx_status fmx_wcomp_proxy(const double* X, const int32_t* pdate, const int32_t* ncol, const int32_t* col,
+                           const int32_t* suf, const int32_t* grp, int32_t KMAX, int64_t J, int64_t D, int64_t A,
+                           const double* lohi, int64_t G, double* Prox, void* stream);
+/* weighted sum of normalised proxies (Python sum, NaN propagates), demean, NaN -> 0,
+ * written to Out[pdate[j]][:]. */
+fmx_status fmx_wcomp_combine(const double* Nrm, const int32_t* pdate, const int32_t* ngrp, const double* gw,
+                             int32_t KMAX, int64_t J, int64_t D, int64_t A, const uint8_t* present, double* Out,
+                             void* stream);
 
 #ifdef __cplusplus
 }

@@ -22,9 +22,10 @@ def fm():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import factormodeling_amd.composite_factor as cf
     import factormodeling_amd.factor_selector as fs
     import factormodeling_amd.operations as ops
-    return ops, fs
+    return ops, fs, cf
 
 
 @pytest.fixture(scope="module", params=["ops_dense.npz", "ops_ragged.npz"])
@@ -209,3 +210,23 @@ def test_corr_gram_vs_oracle(fm):
     np.testing.assert_allclose(C, Cref, rtol=1e-10, atol=1e-12)
     order = list(rng.permutation(F))
     assert E.greedy_prune(C, order, 0.1, 10) == OG.greedy_prune(Cref, order, 0.1, 10)
+
+
+def test_composite_vs_reference(fm):
+    cf = fm[2]
+    st = load("composite.npz")
+    dates, syms, names, df, idx = _factor_frame(st)
+    sels = {"all": names, "sub": [names[i] for i in (0, 1, 2, 5, 6, 7, 9, 11)]}
+    for sk, sel in sels.items():
+        for meth in ("zscore", "rank"):
+            out = cf.composite_factor_calculation(df, sel, method=meth)
+            assert out.name == "composite_factor" and out.index.equals(df.index)
+            assert_close(out.to_numpy(), st[f"out_cfc_{sk}_{meth}"], rtol=RTOL, atol=ATOL, what=f"cfc_{sk}_{meth}")
+    seldf = pd.DataFrame(st["sel_W"], index=pd.DatetimeIndex(pd.to_datetime(st["sel_dates"]), name="date"),
+                         columns=names)
+    for meth in ("zscore", "rank"):
+        out = cf.weighted_composite_factor(df, seldf, method=meth)
+        assert out.name == "composite_factor" and out.index.equals(df.index)
+        assert_close(out.to_numpy(), st[f"out_wcf_{meth}"], rtol=RTOL, atol=ATOL, what=f"wcf_{meth}")
+    with pytest.raises(ValueError):
+        cf.composite_factor_calculation(df, names, method="bogus")
