@@ -483,6 +483,8 @@ extern "C" fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
   FMX_ARG(method >= FMX_RANK_AVERAGE && method <= FMX_RANK_AVERAGE_PROPAGATE, "unknown rank method");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  if (method != FMX_RANK_FIRST && method != FMX_RANK_DENSE)
+    return br_cs_rank(X, Y, F, D, A, ld, method, present, as_stream(stream));
   int P = next_pow2((int)A);
   if (P < 2) P = 2;
   size_t lds = (size_t)P * 10 + 16 + 16 * 4 + 64;
@@ -500,6 +502,7 @@ static fmx_status cs_quantile(int op, const double* X, double* Y, int64_t F, int
   FMX_ARG(X && Y, "null panel");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  if (A <= 16384) return br_cs_quantile(op, X, Y, F, D, A, ld, qlo, qhi, present, as_stream(stream));
   int P = next_pow2((int)A);
   if (P < 2) P = 2;
   size_t lds = (size_t)P * 10 + 16 + 16 * 4 + 16 + 64;

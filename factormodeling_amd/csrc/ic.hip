@@ -235,20 +235,29 @@ __global__ void k_select_icir_top(const double* __restrict__ metrics, int64_t J,
 using namespace fmx;
 
 extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
-                                   const int32_t* lags_dev, int32_t n_lags, double* out, void* stream) {
-  FMX_ARG(X && R && out && lags_dev, "null pointer");
+                                   const int32_t* lags, int32_t n_lags, double* out, void* stream) {
+  FMX_ARG(X && R && out && lags, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
   FMX_ARG(n_lags >= 1 && n_lags <= 8, "n_lags");
+  for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
   if (F == 0 || D == 0) return FMX_OK;
+  if (A <= 16384) return br_ic_daily(X, R, F, D, A, ld, lags, n_lags, out, as_stream(stream));
+  // very wide rows: one LDS-bitonic workgroup per (factor, date, lag)
   int P = next_pow2((int)std::max<int64_t>(A, 2));
   size_t lds = (size_t)P * 10 + 16 + 16 * 8 + 16 * 4 + 64;
-  if (lds > 160 * 1024) { set_error("A too large for LDS sort"); return FMX_ERR_UNSUPPORTED; }
+  if (lds > 160 * 1024) { set_error("A too large for the IC kernels"); return FMX_ERR_UNSUPPORTED; }
+  int32_t* lags_dev = nullptr;
+  hipStream_t st = as_stream(stream);
+  FMX_HIP(hipMallocAsync((void**)&lags_dev, sizeof(int32_t) * n_lags, st));
+  FMX_HIP(hipMemcpyAsync(lags_dev, lags, sizeof(int32_t) * n_lags, hipMemcpyHostToDevice, st));
+  FMX_HIP(hipStreamSynchronize(st));
   if (lds > 64 * 1024)
     FMX_HIP(hipFuncSetAttribute((const void*)k_ic_daily, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {(void*)&X, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&lags_dev, (void*)&P,
                   (void*)&out};
   FMX_HIP(hipLaunchKernel((const void*)k_ic_daily, dim3((unsigned)D, (unsigned)F, (unsigned)n_lags), dim3(IC_NT),
-                          args, lds, as_stream(stream)));
+                          args, lds, st));
+  FMX_HIP(hipFreeAsync(lags_dev, st));
   return FMX_OK;
 }
 

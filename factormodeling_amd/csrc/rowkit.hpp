@@ -243,4 +243,12 @@ struct PwTable {
 // Host: schedule table covering every n <= nmax on the current device (capi.hip).
 PwTable pw_table(int nmax, fmx_status* err);
 
+// Host: bucket-rank launchers (rank_ops.hip).
+fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
+                      const uint8_t* present, hipStream_t st);
+fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                          double qlo, double qhi, const uint8_t* present, hipStream_t st);
+fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
+                       const int32_t* lags_host, int n_lags, double* out, hipStream_t st);
+
 }  // namespace fmx

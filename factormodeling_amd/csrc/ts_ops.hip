@@ -17,6 +17,8 @@
 // (roll_sum / roll_mean / roll_var incl. Kahan compensation, the consecutive-same-
 // value guard and zsqrt), so with -ffp-contract=off the outputs are bit-identical to
 // pandas.
+#include <cstdlib>
+
 #include "fmx_common.hpp"
 
 namespace fmx {
@@ -130,119 +132,142 @@ struct VarSt {
 __device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v); }
 
 // ------------------------------------------------------------------------------------
-// Generic walker: calls body(d, v) for each present row of the lane's column, with up
-// to TS_UNROLL loads in flight.
-template <class Body>
-__device__ __forceinline__ void walk_column(const double* __restrict__ x, double* __restrict__ y,
-                                            int64_t D, int64_t ld, const uint8_t* __restrict__ pres,
-                                            Body&& body) {
-  for (int64_t d0 = 0; d0 < D; d0 += TS_UNROLL) {
-    double v[TS_UNROLL];
-    uint8_t p[TS_UNROLL];
-#pragma unroll
-    for (int u = 0; u < TS_UNROLL; ++u) {
-      int64_t d = d0 + u;
-      if (d < D) {
-        v[u] = x[d * ld];
-        p[u] = pres ? pres[d * ld] : 1;
-      } else {
-        p[u] = 0;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < TS_UNROLL; ++u) {
-      int64_t d = d0 + u;
-      if (d < D) {
-        if (p[u]) y[d * ld] = body(d, v[u]);
-        else y[d * ld] = qnan();
-      }
-    }
+// Per-column walker state.  i counts the column's present rows; the column's window lives
+// in the LDS ring at ring[(slot * TS_BLOCK + lane) * V + u].
+struct ColState {
+  SumSt ss;
+  MeanSt ms;
+  VarSt vs;
+  double last;
+  int64_t i;
+  int slot, nan_in_win;
+  bool first;
+  __device__ void init() { i = 0; slot = 0; nan_in_win = 0; first = true; last = qnan(); }
+};
+
+template <int OP, int V>
+__device__ __forceinline__ double ts_step(ColState& c, double v, int W, double* ring, int lane, int u) {
+  if (c.first) { c.ss.init(v); c.ms.init(v); c.vs.init(v); c.first = false; }
+  double old = qnan();
+  if (OP != FMX_TS_BACKFILL) {
+    double* rs = ring + ((int64_t)c.slot * TS_BLOCK + lane) * V + u;
+    if (c.i >= W) old = *rs;
+    *rs = v;
+    c.slot = (c.slot + 1 == W) ? 0 : c.slot + 1;
   }
+  double out;
+  if (OP == FMX_TS_SUM) {
+    if (c.i >= W) c.ss.remove(old);
+    c.ss.add(v);
+    out = c.ss.result(W);
+  } else if (OP == FMX_TS_MEAN) {
+    if (c.i >= W) c.ms.remove(old);
+    c.ms.add(v);
+    out = c.ms.result(W);
+  } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
+    if (c.i >= W) c.vs.remove(old);
+    c.vs.add(v);
+    const double var = c.vs.var(W, 1);
+    out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
+  } else if (OP == FMX_TS_ZSCORE) {
+    if (c.i >= W) { c.ms.remove(old); c.vs.remove(old); }
+    c.ms.add(v); c.vs.add(v);
+    const double m = c.ms.result(W);
+    double sd = zsqrt(c.vs.var(W, 1));
+    if (sd == 0.0) sd = qnan();
+    out = (v - m) / sd;
+  } else if (OP == FMX_TS_RANK || OP == FMX_TS_DECAY) {
+    if (c.i >= W && old != old) c.nan_in_win -= 1;
+    if (v != v) c.nan_in_win += 1;
+    if (c.i + 1 < W || c.nan_in_win > 0) {
+      out = qnan();
+    } else if (OP == FMX_TS_RANK) {
+      int less = 0, eq = 0;
+      for (int k = 0; k < W; ++k) {
+        const double w = ring[((int64_t)k * TS_BLOCK + lane) * V + u];
+        less += (w < v);
+        eq += (w == v);
+      }
+      out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
+    } else {
+      // oldest element sits at `slot` (just advanced); weights 1..W oldest->newest
+      double acc = 0.0;
+      int sl = c.slot;
+      for (int k = 1; k <= W; ++k) {
+        acc += ring[((int64_t)sl * TS_BLOCK + lane) * V + u] * (double)k;
+        sl = (sl + 1 == W) ? 0 : sl + 1;
+      }
+      out = acc / ((double)W * (double)(W + 1) / 2.0);
+    }
+  } else if (OP == FMX_TS_DIFF) {
+    out = (c.i >= W) ? v - old : qnan();
+  } else if (OP == FMX_TS_DELAY) {
+    out = (c.i >= W) ? old : qnan();
+  } else {  // BACKFILL
+    if (v == v) c.last = v;
+    out = c.last;
+  }
+  c.i += 1;
+  return out;
 }
 
-template <int OP>
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+// One lane owns V adjacent assets of one factor (V = 2: 16-byte loads/stores) and walks
+// the dates with TS_UNROLL rows of loads in flight.
+template <int OP, int V>
 __global__ void __launch_bounds__(TS_BLOCK)
 k_ts(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
      int W, const uint8_t* __restrict__ present) {
-  extern __shared__ double ring[];  // [W][TS_BLOCK]
+  extern __shared__ double ring[];  // [W][TS_BLOCK][V]
   const int lane = threadIdx.x;
-  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+  const int64_t a = ((int64_t)blockIdx.x * TS_BLOCK + lane) * V;
   if (a >= A) return;
   const int64_t f = blockIdx.y;
   const double* x = X + f * D * ld + a;
   double* y = Y + f * D * ld + a;
   const uint8_t* pres = present ? present + a : nullptr;
-
-  int64_t i = 0;  // present-row counter
-  int slot = 0;
-  int nan_in_win = 0;
-  SumSt ss; MeanSt ms; VarSt vs; double last = qnan();
-  bool first = true;
-
-  walk_column(x, y, D, ld, pres, [&](int64_t d, double v) -> double {
-    (void)d;
-    if (first) { ss.init(v); ms.init(v); vs.init(v); first = false; }
-    double old = qnan();
-    if (OP != FMX_TS_BACKFILL) {
-      if (i >= W) old = ring[slot * TS_BLOCK + lane];
-      ring[slot * TS_BLOCK + lane] = v;
-      slot = (slot + 1 == W) ? 0 : slot + 1;
-    }
-    double out;
-    if (OP == FMX_TS_SUM) {
-      if (i >= W) ss.remove(old);
-      ss.add(v);
-      out = ss.result(W);
-    } else if (OP == FMX_TS_MEAN) {
-      if (i >= W) ms.remove(old);
-      ms.add(v);
-      out = ms.result(W);
-    } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
-      if (i >= W) vs.remove(old);
-      vs.add(v);
-      double var = vs.var(W, 1);
-      out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
-    } else if (OP == FMX_TS_ZSCORE) {
-      if (i >= W) { ms.remove(old); vs.remove(old); }
-      ms.add(v); vs.add(v);
-      double m = ms.result(W);
-      double s = zsqrt(vs.var(W, 1));
-      if (s == 0.0) s = qnan();
-      out = (v - m) / s;
-    } else if (OP == FMX_TS_RANK || OP == FMX_TS_DECAY) {
-      if (i >= W && old != old) nan_in_win -= 1;
-      if (v != v) nan_in_win += 1;
-      if (i + 1 < W || nan_in_win > 0) {
-        out = qnan();
-      } else if (OP == FMX_TS_RANK) {
-        int less = 0, eq = 0;
-        for (int k = 0; k < W; ++k) {
-          double u = ring[k * TS_BLOCK + lane];
-          less += (u < v);
-          eq += (u == v);
+  ColState cs[V];
+#pragma unroll
+  for (int u = 0; u < V; ++u) cs[u].init();
+  for (int64_t d0 = 0; d0 < D; d0 += TS_UNROLL) {
+    double v[TS_UNROLL][V];
+    uint8_t p[TS_UNROLL][V];
+#pragma unroll
+    for (int q = 0; q < TS_UNROLL; ++q) {
+      const int64_t d = d0 + q;
+      if (d < D) {
+        if (V == 2) {
+          const dbl2 t = *reinterpret_cast<const dbl2*>(x + d * ld);
+          v[q][0] = t[0];
+          v[q][V - 1] = t[1];
+        } else {
+          v[q][0] = x[d * ld];
         }
-        out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
+#pragma unroll
+        for (int u = 0; u < V; ++u) p[q][u] = pres ? pres[d * ld + u] : 1;
       } else {
-        // oldest element sits at `slot` (just advanced); weights 1..W oldest->newest
-        double acc = 0.0;
-        int s = slot;
-        for (int k = 1; k <= W; ++k) {
-          acc += ring[s * TS_BLOCK + lane] * (double)k;
-          s = (s + 1 == W) ? 0 : s + 1;
-        }
-        out = acc / ((double)W * (double)(W + 1) / 2.0);
+#pragma unroll
+        for (int u = 0; u < V; ++u) p[q][u] = 0;
       }
-    } else if (OP == FMX_TS_DIFF) {
-      out = (i >= W) ? v - old : qnan();
-    } else if (OP == FMX_TS_DELAY) {
-      out = (i >= W) ? old : qnan();
-    } else {  // BACKFILL
-      if (v == v) last = v;
-      out = last;
     }
-    i += 1;
-    return out;
-  });
+#pragma unroll
+    for (int q = 0; q < TS_UNROLL; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) continue;
+      double o[V];
+#pragma unroll
+      for (int u = 0; u < V; ++u) o[u] = p[q][u] ? ts_step<OP, V>(cs[u], v[q][u], W, ring, lane, u) : qnan();
+      if (V == 2) {
+        dbl2 t;
+        t[0] = o[0];
+        t[1] = o[V - 1];
+        *reinterpret_cast<dbl2*>(y + d * ld) = t;
+      } else {
+        y[d * ld] = o[0];
+      }
+    }
+  }
 }
 
 // W == 0: diff -> x - x, delay -> x, decay -> x (no ring).
@@ -429,9 +454,14 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
     FMX_LAUNCH_CHECK("k_ts_window0");
     return FMX_OK;
   }
-  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
+  // two adjacent assets per lane (16-byte accesses) when rows stay 16-byte aligned
+  const bool v2 = (ld % 2 == 0) && (A % 2 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0) &&
+                  (getenv("FMX_TS_V1") == nullptr);
+  const int V = v2 ? 2 : 1;
+  dim3 grid((unsigned)ceil_div(A, TS_BLOCK * V), (unsigned)F);
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&W, (void*)&present};
   if ((op == FMX_TS_DIFF || op == FMX_TS_DELAY) && W < 0) {
+    grid = dim3((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
     int K = -W;
     size_t lds = (size_t)2 * K * TS_BLOCK * sizeof(double);
     const void* k = op == FMX_TS_DIFF ? (const void*)k_ts_lead<FMX_TS_DIFF> : (const void*)k_ts_lead<FMX_TS_DELAY>;
@@ -439,20 +469,22 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
     return launch_ring(k, grid, lds, st, largs);
   }
   FMX_ARG(W >= 1, "window must be >= 1");
-  size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * sizeof(double);
+  size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * V * sizeof(double);
   const void* k = nullptr;
+#define FMX_TSK(O) (V == 2 ? (const void*)k_ts<O, 2> : (const void*)k_ts<O, 1>)
   switch (op) {
-    case FMX_TS_SUM: k = (const void*)k_ts<FMX_TS_SUM>; break;
-    case FMX_TS_MEAN: k = (const void*)k_ts<FMX_TS_MEAN>; break;
-    case FMX_TS_STD: k = (const void*)k_ts<FMX_TS_STD>; break;
-    case FMX_TS_VAR: k = (const void*)k_ts<FMX_TS_VAR>; break;
-    case FMX_TS_ZSCORE: k = (const void*)k_ts<FMX_TS_ZSCORE>; break;
-    case FMX_TS_RANK: k = (const void*)k_ts<FMX_TS_RANK>; break;
-    case FMX_TS_DECAY: k = (const void*)k_ts<FMX_TS_DECAY>; break;
-    case FMX_TS_DIFF: k = (const void*)k_ts<FMX_TS_DIFF>; break;
-    case FMX_TS_DELAY: k = (const void*)k_ts<FMX_TS_DELAY>; break;
-    default: k = (const void*)k_ts<FMX_TS_BACKFILL>; break;
+    case FMX_TS_SUM: k = FMX_TSK(FMX_TS_SUM); break;
+    case FMX_TS_MEAN: k = FMX_TSK(FMX_TS_MEAN); break;
+    case FMX_TS_STD: k = FMX_TSK(FMX_TS_STD); break;
+    case FMX_TS_VAR: k = FMX_TSK(FMX_TS_VAR); break;
+    case FMX_TS_ZSCORE: k = FMX_TSK(FMX_TS_ZSCORE); break;
+    case FMX_TS_RANK: k = FMX_TSK(FMX_TS_RANK); break;
+    case FMX_TS_DECAY: k = FMX_TSK(FMX_TS_DECAY); break;
+    case FMX_TS_DIFF: k = FMX_TSK(FMX_TS_DIFF); break;
+    case FMX_TS_DELAY: k = FMX_TSK(FMX_TS_DELAY); break;
+    default: k = FMX_TSK(FMX_TS_BACKFILL); break;
   }
+#undef FMX_TSK
   return launch_ring(k, grid, lds, st, args);
 }
 

@@ -173,9 +173,10 @@ def ic_daily(X, R, lags=(1,)):
     F, D, A = X.shape
     if tuple(R.shape) != (D, A) or R.dtype != F64 or not R.is_contiguous():
         raise _lib.FmxError("R must be a contiguous float64 [D][A] device tensor")
-    lag_t = torch.tensor(list(lags), dtype=torch.int32, device=X.device)
+    lag_h = (ctypes.c_int32 * len(lags))(*[int(v) for v in lags])
     out = torch.empty((len(lags), 4, F, D), dtype=F64, device=X.device)
-    call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ptr(lag_t), len(lags), ptr(out), stream_ptr())
+    call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p), len(lags), ptr(out),
+         stream_ptr())
     return out
 
 
@@ -206,7 +207,7 @@ def zscore_exposures(X):
     _check_panel(X)
     F, D, A = X.shape
     Z = torch.empty_like(X)
-    M = torch.empty_like(X)
+    M = torch.empty(X.shape, dtype=torch.bfloat16, device=X.device)   # 0/1 validity
     call("fmx_zscore_exposures", ptr(X), ptr(Z), ptr(M), F, D, A, A, stream_ptr())
     return Z, M
 

@@ -143,13 +143,16 @@ class EngineBackend:
 ENGINE = EngineBackend()
 
 
-def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE):
-    """Operator set over the local panel (halo rows included as warm-up)."""
+def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE, collect=None, own=slice(None)):
+    """Operator set over the local panel (halo rows included as warm-up).  ``collect``
+    (a dict) receives a copy of every operator's owned-date output (tests only)."""
     Y = out if out is not None else torch.empty_like(X)
     for kind, op, w in cfg.ops:
         t0 = _ev(timers)
         be.op(kind, op, w, X, Y)
         _rec(timers, f"{kind}:{op or ''}:{w or ''}", t0)
+        if collect is not None:
+            collect[f"{kind}:{op or ''}:{w or ''}"] = Y[:, own].clone()
     return Y
 
 
@@ -169,13 +172,13 @@ def _rec(timers, name, t0):
     timers.append((name, t0, e))
 
 
-def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE):
+def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=None):
     """One pass of the hot path.  Returns (selected weights [J][F] (every rank holds the
-    full result), kept factor list)."""
+    full result), kept factor list).  ``collect`` (tests) receives intermediate results."""
     t0 = _ev(timers)
     sp.exchange_halo()
     _rec(timers, "halo", t0)
-    run_ops(sp.X, cfg, timers=timers, be=be)
+    run_ops(sp.X, cfg, timers=timers, be=be, collect=collect, own=slice(sp.halo, None))
     # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     daily = be.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
@@ -214,6 +217,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE):
     full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
     kept = be.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, cfg.top_x)
     _rec(timers, "prune", t0)
+    if collect is not None:
+        collect.update(daily=full, summ=summ, win=win, C=C)
     return w, kept
 
 

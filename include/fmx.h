@@ -138,10 +138,11 @@ fmx_status fmx_bucket(const double* X, int32_t* codes, int64_t n, const double* 
                       void* stream);
 
 /* ---- IC, metrics, selection (factor_selector.py:26-139, factor_selection_methods.py:6-26) */
-/* Daily stats for each lag in lags_dev[0..n_lags) (device int32): pairs (X[f][t-L], R[t]).
- * out: [n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta); NaN where undefined. */
+/* Daily stats for each lag in lags[0..n_lags) (HOST int32 array, lags >= 0): pairs
+ * (X[f][t-L], R[t]).  out: [n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta); NaN where
+ * undefined.  Each exposure row is ranked once for up to two lags. */
 fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
-                        const int32_t* lags_dev, int32_t n_lags, double* out, void* stream);
+                        const int32_t* lags, int32_t n_lags, double* out, void* stream);
 /* Window summaries of one lag's daily stats [4][F][D] over J date windows [d0, d1).
  * out: [J][F][8] = IC, IC_IR, rank_IC, rank_IC_IR, tstat, n_beta, pct_pos, n_days. */
 fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev, const int32_t* d1_dev,
@@ -152,12 +153,14 @@ fmx_status fmx_select_icir_top(const double* metrics, int64_t J, int64_t F, int3
                                double threshold, int32_t top_x, int32_t* order_out, double* w_out, void* stream);
 
 /* ---- factor correlation GEMM (builder-defined) ------------------------ */
-/* Z, M: per-date z-scored exposures and validity (0/1) as float64 [F][D][ld]. */
-fmx_status fmx_zscore_exposures(const double* X, double* Z, double* M, int64_t F, int64_t D, int64_t A,
+/* Z: per-date z-scored exposures (float64 [F][D][ld], NaN -> 0); M: validity as bf16
+ * 0/1 (uint16 bit patterns [F][D][ld]). */
+fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
                                 int64_t ld, void* stream);
-/* G[F][F] += sum_{d in [d0,d1), a} Z[i][d][a] Z[j][d][a] and N[F][F] likewise for M,
- * on fp64 MFMA (v_mfma_f64_16x16x4_f64).  accumulate = 0 overwrites. */
-fmx_status fmx_gram(const double* Z, const double* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
+/* G[F][F] (+)= sum_{d in [d0,d1), a} Z[i][d][a] Z[j][d][a] on fp64 MFMA
+ * (v_mfma_f64_16x16x4_f64) and N[F][F] (+)= the same sum over M on bf16 MFMA (exact
+ * pair counts).  accumulate = 0 overwrites.  M/N may be NULL. */
+fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
                     int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
 
 /* ---- composite factors (composite_factor.py:137-342) ------------------------------- */
