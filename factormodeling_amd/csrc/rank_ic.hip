@@ -1,0 +1,43 @@
+// Fused two-lag daily IC launcher (rank_kernels.hpp).
+// Reference: factor_selector.py:36-48
+#include "rank_launch.hpp"
+
+namespace fmx {
+
+// dates t < L get an empty record (n = 0, NaN stats)
+__global__ void k_ic_empty(double* out, int64_t F, int64_t D, int L0, int L1, int NL) {
+  const int64_t f = blockIdx.x;
+  for (int m = 0; m < NL; ++m) {
+    const int L = m == 0 ? L0 : L1;
+    for (int64_t td = threadIdx.x; td < min<int64_t>(L, D); td += blockDim.x) {
+      double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
+      o[0] = 0.0;
+      o[F * D] = qnan();
+      o[2 * F * D] = qnan();
+      o[3 * F * D] = qnan();
+    }
+  }
+}
+
+
+fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
+                       const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
+  const int nt = br_nt(1024);
+  const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8 + (size_t)((A + 15) & ~15ll);
+  for (int base = 0; base < n_lags; base += 2) {
+    int NL = std::min(2, n_lags - base);
+    int L0 = lags_host[base], L1 = NL > 1 ? lags_host[base + 1] : 0;
+    double* o = out + (int64_t)base * 4 * F * D;
+    k_ic_empty<<<(unsigned)F, 64, 0, st>>>(o, F, D, L0, L1, NL);
+    FMX_LAUNCH_CHECK("k_ic_empty");
+    void* args[] = {(void*)&X, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0, (void*)&L1,
+                    (void*)&NL, (void*)&o};
+    fmx_status e = launch_br(FMX_EMAX_TABLE(k_ic_daily_br), nt, A, F * D, lds, args, st);
+    if (e) return e;
+  }
+  return FMX_OK;
+}
+
+}  // namespace fmx
+
+BR_PHASE_EXPORT(fmx_debug_phase_ic)

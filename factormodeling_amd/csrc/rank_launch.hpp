@@ -1,0 +1,64 @@
+// Launch plumbing shared by the bucket-rank translation units (rank_cs.hip,
+// rank_q.hip, rank_ic.hip): row-length -> EMAX table, workgroup size choice.
+#pragma once
+#include <cstdlib>
+#include "rank_kernels.hpp"
+
+namespace fmx {
+
+static inline int br_emax(int64_t A, int nt) {
+  const int64_t e = ceil_div(std::max<int64_t>(A, 1), nt);
+  static const int tab[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32};
+  for (int v : tab)
+    if (e <= v && (int64_t)v * nt <= 16384) return v;
+  return -1;
+}
+
+// Workgroup size of a row kernel: its measured best (cs_rank and the IC 1024, the quantile
+// kernels 512 on MI355X at A = 5000), or FMX_BR_NT=512|1024 for all of them.
+static inline int br_nt(int preferred) {
+  static int forced = [] {
+    const char* e = getenv("FMX_BR_NT");
+    const int v = e ? atoi(e) : 0;
+    return (v == 512 || v == 1024) ? v : 0;
+  }();
+  return forced ? forced : preferred;
+}
+
+template <class K>
+static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblocks, size_t lds, void** args,
+                                   hipStream_t st) {
+  const void* k = kern_table(nt, br_emax(A, nt));
+  if (!k) { set_error("row too long for the bucket-rank kernels (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
+  if (nblocks <= 0) return FMX_OK;
+  if (nblocks > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nblocks), dim3(nt), args, lds, st));
+  return FMX_OK;
+}
+
+#define FMX_EMAX_CASES(KT, NT)                                               \
+  switch (E) {                                                               \
+    case 1: return (const void*)KT<NT, 1>;                                   \
+    case 2: return (const void*)KT<NT, 2>;                                   \
+    case 3: return (const void*)KT<NT, 3>;                                   \
+    case 4: return (const void*)KT<NT, 4>;                                   \
+    case 5: return (const void*)KT<NT, 5>;                                   \
+    case 6: return (const void*)KT<NT, 6>;                                   \
+    case 8: return (const void*)KT<NT, 8>;                                   \
+    case 10: return (const void*)KT<NT, 10>;                                 \
+    case 12: return (const void*)KT<NT, 12>;                                 \
+    case 16: return (const void*)KT<NT, 16>;                                 \
+    case 20: return (const void*)KT<NT, 20>;                                 \
+    case 24: return (const void*)KT<NT, 24>;                                 \
+    case 32: return (const void*)KT<NT, 32>;                                 \
+    default: return (const void*)nullptr;                                    \
+  }
+
+#define FMX_EMAX_TABLE(KT)                                                   \
+  [](int nt, int E) -> const void* {                                         \
+    if (nt == 512) { FMX_EMAX_CASES(KT, 512) }                               \
+    FMX_EMAX_CASES(KT, 1024)                                                 \
+  }
+
+}  // namespace fmx

@@ -28,7 +28,7 @@ constexpr int TS_UNROLL = 8;   // dates prefetched per lane
 
 struct SumSt {
   double s, ca, cr, prev;
-  int64_t n, same;
+  int n, same;                 // counts fit 32 bits (n <= D)
   __device__ void init(double first) { s = ca = cr = 0.0; n = 0; same = 0; prev = first; }
   __device__ void add(double v) {
     if (v == v) {
@@ -55,7 +55,7 @@ struct SumSt {
 
 struct MeanSt {
   double s, ca, cr, prev;
-  int64_t n, neg, same;
+  int n, neg, same;
   __device__ void init(double first) { s = ca = cr = 0.0; n = neg = same = 0; prev = first; }
   __device__ void add(double v) {
     if (v == v) {
@@ -89,7 +89,7 @@ struct MeanSt {
 
 struct VarSt {
   double mean, ssq, n, ca, cr, prev;
-  int64_t same;
+  int same;
   __device__ void init(double first) { mean = ssq = n = ca = cr = 0.0; same = 0; prev = first; }
   __device__ void add(double v) {
     if (v != v) return;
@@ -209,6 +209,120 @@ __device__ __forceinline__ double ts_step(ColState& c, double v, int W, double* 
   }
   c.i += 1;
   return out;
+}
+
+// One rolling step with the window ring in registers: slot q is a compile-time index (the
+// caller unrolls its date loop by W), so ring[] stays in VGPRs.  Same state machines and
+// operation order as ts_step.
+template <int OP, int W>
+__device__ __forceinline__ double ts_step_reg(ColState& c, double v, double* ring, int q) {
+  if (c.first) { c.ss.init(v); c.ms.init(v); c.vs.init(v); c.first = false; }
+  double old = qnan();
+  if (OP != FMX_TS_BACKFILL) {
+    if (c.i >= W) old = ring[q];
+    ring[q] = v;
+  }
+  double out;
+  if (OP == FMX_TS_SUM) {
+    if (c.i >= W) c.ss.remove(old);
+    c.ss.add(v);
+    out = c.ss.result(W);
+  } else if (OP == FMX_TS_MEAN) {
+    if (c.i >= W) c.ms.remove(old);
+    c.ms.add(v);
+    out = c.ms.result(W);
+  } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
+    if (c.i >= W) c.vs.remove(old);
+    c.vs.add(v);
+    const double var = c.vs.var(W, 1);
+    out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
+  } else if (OP == FMX_TS_ZSCORE) {
+    if (c.i >= W) { c.ms.remove(old); c.vs.remove(old); }
+    c.ms.add(v); c.vs.add(v);
+    const double m = c.ms.result(W);
+    double sd = zsqrt(c.vs.var(W, 1));
+    if (sd == 0.0) sd = qnan();
+    out = (v - m) / sd;
+  } else if (OP == FMX_TS_RANK || OP == FMX_TS_DECAY) {
+    if (c.i >= W && old != old) c.nan_in_win -= 1;
+    if (v != v) c.nan_in_win += 1;
+    if (c.i + 1 < W || c.nan_in_win > 0) {
+      out = qnan();
+    } else if (OP == FMX_TS_RANK) {
+      int less = 0, eq = 0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        less += (ring[k] < v);
+        eq += (ring[k] == v);
+      }
+      out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
+    } else {
+      // oldest element sits in slot q+1 (mod W); weights 1..W oldest->newest
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 1; k <= W; ++k) acc += ring[(q + k) % W] * (double)k;
+      out = acc / ((double)W * (double)(W + 1) / 2.0);
+    }
+  } else if (OP == FMX_TS_DIFF) {
+    out = (c.i >= W) ? v - old : qnan();
+  } else if (OP == FMX_TS_DELAY) {
+    out = (c.i >= W) ? old : qnan();
+  } else {  // BACKFILL
+    if (v == v) c.last = v;
+    out = c.last;
+  }
+  c.i += 1;
+  return out;
+}
+
+// Dense panels (no presence mask), W in the instantiated set: one lane per (factor,
+// asset) column, 256 columns per block; the date loop is unrolled by W so that the ring
+// slot of each unrolled step is static, and loads run PF dates ahead (PF divides W).
+// Without an LDS ring, occupancy is set by registers alone.
+template <int OP, int W, int PF>
+__global__ void __launch_bounds__(256, (OP == FMX_TS_SUM || OP == FMX_TS_ZSCORE) ? 4 : 5)
+k_ts_reg(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld) {
+  static_assert(W % PF == 0, "PF must divide W");
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  ColState c;
+  c.init();
+  double ring[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) ring[q] = 0.0;
+  double pf[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) pf[q] = q < D ? x[q * ld] : 0.0;
+  const double* xp = x + PF * ld;     // next date to fetch
+  double* yp = y;                     // next date to store
+  int64_t d0 = 0;
+  // full blocks of W dates whose prefetches stay in range: no bounds checks
+  for (; d0 + W + PF <= D; d0 += W) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const double v = pf[q % PF];
+      pf[q % PF] = *xp;
+      xp += ld;
+      *yp = ts_step_reg<OP, W>(c, v, ring, q);
+      yp += ld;
+    }
+  }
+  for (; d0 < D; d0 += W) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const int64_t d = d0 + q;
+      if (d < D) {
+        const double v = pf[q % PF];
+        if (d + PF < D) pf[q % PF] = *xp;
+        xp += ld;
+        *yp = ts_step_reg<OP, W>(c, v, ring, q);
+        yp += ld;
+      }
+    }
+  }
 }
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -416,6 +530,32 @@ k_ts_regression(const double* __restrict__ Yv, const double* __restrict__ Xv,
   }
 }
 
+// Register-ring kernel for (op, W), or nullptr when W is not an instantiated window.
+template <int W, int PF>
+static const void* ts_reg_for(int op) {
+  switch (op) {
+    case FMX_TS_SUM: return (const void*)k_ts_reg<FMX_TS_SUM, W, PF>;
+    case FMX_TS_MEAN: return (const void*)k_ts_reg<FMX_TS_MEAN, W, PF>;
+    case FMX_TS_STD: return (const void*)k_ts_reg<FMX_TS_STD, W, PF>;
+    case FMX_TS_VAR: return (const void*)k_ts_reg<FMX_TS_VAR, W, PF>;
+    case FMX_TS_ZSCORE: return (const void*)k_ts_reg<FMX_TS_ZSCORE, W, PF>;
+    case FMX_TS_RANK: return (const void*)k_ts_reg<FMX_TS_RANK, W, PF>;
+    case FMX_TS_DECAY: return (const void*)k_ts_reg<FMX_TS_DECAY, W, PF>;
+    case FMX_TS_DIFF: return (const void*)k_ts_reg<FMX_TS_DIFF, W, PF>;
+    case FMX_TS_DELAY: return (const void*)k_ts_reg<FMX_TS_DELAY, W, PF>;
+    default: return nullptr;
+  }
+}
+
+static const void* ts_reg_kernel(int op, int W) {
+  switch (W) {
+    case 5: return ts_reg_for<5, 5>(op);
+    case 10: return ts_reg_for<10, 10>(op);
+    case 20: return ts_reg_for<20, 5>(op);
+    default: return nullptr;
+  }
+}
+
 static fmx_status launch_ring(const void* kern, dim3 grid, size_t lds, hipStream_t st, void** args) {
   if (lds > 160 * 1024) {
     set_error("window too large for the LDS ring (needs " + std::to_string(lds) + " bytes)");
@@ -469,6 +609,14 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
     return launch_ring(k, grid, lds, st, largs);
   }
   FMX_ARG(W >= 1, "window must be >= 1");
+  if (!present && op != FMX_TS_BACKFILL && getenv("FMX_TS_LDS") == nullptr) {
+    const void* kr = ts_reg_kernel(op, W);
+    if (kr) {
+      void* rargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld};
+      FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, st));
+      return FMX_OK;
+    }
+  }
   size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * V * sizeof(double);
   const void* k = nullptr;
 #define FMX_TSK(O) (V == 2 ? (const void*)k_ts<O, 2> : (const void*)k_ts<O, 1>)
