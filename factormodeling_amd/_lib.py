@@ -27,6 +27,7 @@ SIGNATURES = {
     "fmx_ts_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_ts_regression": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp],
     "fmx_cs_moment": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
+    "fmx_cs_moment_stats": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
     "fmx_cs_filter_center": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
@@ -39,6 +40,7 @@ SIGNATURES = {
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
+    "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
     "fmx_comp_adj": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
     "fmx_comp_proxy": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
@@ -51,7 +53,7 @@ _RESTYPES = {"fmx_last_error": c_cp}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)
-CS = dict(zscore=0, mean=1, market_neutralize=2)
+CS = dict(zscore=0, mean=1, market_neutralize=2, stats=3)
 RANK = dict(average=0, min=1, max=2, first=3, dense=4, scipy_average=5)
 GROUP = dict(mean=0, neutralize=1, normalize=2, rank=3)
 EW = dict(sign=0, power=1, log=2, abs=3, clip=4, where=5)

@@ -41,45 +41,83 @@ __device__ int stage_row(const double* __restrict__ x, const uint8_t* __restrict
   return tot;
 }
 
+// stage_row for an NT-thread block (ragged rows only).
+template <int NT>
+__device__ int stage_row_nt(const double* __restrict__ x, const uint8_t* __restrict__ prow, int64_t A, double* v,
+                            uint16_t* pos, int* iscr) {
+  const int64_t C = (A + NT - 1) / NT;
+  const int64_t a0 = threadIdx.x * C, a1 = min<int64_t>(A, a0 + C);
+  int cnt = 0;
+  for (int64_t a = a0; a < a1; ++a) cnt += prow[a] != 0;
+  int tot;
+  int base = block_exscan<NT>(cnt, iscr, &tot);
+  for (int64_t a = a0; a < a1; ++a) {
+    if (prow[a]) {
+      v[base] = x[a];
+      if (pos) pos[base] = (uint16_t)a;
+      ++base;
+    }
+  }
+  __syncthreads();
+  return tot;
+}
+
 // ------------------------------------------------------------------------------------
-// cs_zscore / cs_mean / market_neutralize (nanops.nanmean / nanvar(ddof=0), pairwise)
+// cs_zscore / cs_mean / market_neutralize (nanops.nanmean / nanvar(ddof=0), pairwise).
+// 512 threads per row; the two numpy pairwise sums use block_pw_sum_w0 (wave 0 walks the
+// combine rounds), so a row costs five block barriers.  Optional stats[row] = (mean, sd)
+// (sd = sqrt(nanvar ddof=0); the builder's Gram z-score, oracle/gram.py); OP
+// FMX_CS_STATS_ONLY writes only the stats.
+constexpr int FMX_CS_STATS_ONLY = 3;
+constexpr int CSM_NT = 512;
+
 template <int OP>
-__global__ void __launch_bounds__(CS_NT)
+__global__ void __launch_bounds__(CSM_NT)
 k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
-            const uint8_t* __restrict__ present, PwTable pw) {
+            const uint8_t* __restrict__ present, PwTable pw, double* __restrict__ stats) {
   extern __shared__ double lds[];
-  const int64_t d = blockIdx.x, f = blockIdx.y;
-  const double* x = X + (f * D + d) * ld;
-  double* y = Y + (f * D + d) * ld;
+  const int64_t row = blockIdx.x;
+  const int64_t d = row % D;
+  const double* x = X + row * ld;
+  double* y = Y ? Y + row * ld : nullptr;
   const uint8_t* prow = present ? present + d * ld : nullptr;
   double* v = lds;                                   // [A]
   uint16_t* pos = present ? (uint16_t*)(v + A) : nullptr;
   double* nodes = (double*)((char*)(v + A) + (present ? ((A * 2 + 15) & ~15) : 0));  // [2A/64+8]
   int* iscr = (int*)(nodes + (2 * (A / 64) + 8));
-  double* dscr = (double*)(iscr + 16);
-  const int n = stage_row(x, prow, A, v, pos, iscr);
-  if (n == 0) return;
+  int n;
+  if (!prow) {
+    for (int64_t i = threadIdx.x; i < A; i += CSM_NT) v[i] = x[i];
+    __syncthreads();
+    n = (int)A;
+  } else {
+    n = stage_row_nt<CSM_NT>(x, prow, A, v, pos, iscr);
+  }
+  if (n == 0) {
+    if (stats && threadIdx.x == 0) { stats[2 * row] = qnan(); stats[2 * row + 1] = qnan(); }
+    return;
+  }
   const int32_t* sch = pw.get(n);
-  int c = 0;
-  for (int i = threadIdx.x; i < n; i += CS_NT) c += (v[i] == v[i]);
   int cnt;
-  block_exscan<CS_NT>(c, iscr, &cnt);
-  double s1 = block_pw_sum<CS_NT>([&](int i) { double t = v[i]; return t == t ? t : 0.0; }, sch, nodes);
-  double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+  const double s1 = block_pw_sum_w0<CSM_NT>([&](int i) { double t = v[i]; return t == t ? t : 0.0; },
+                                            [&](int i) { return (int)(v[i] == v[i]); }, sch, nodes, iscr, &cnt);
+  const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
   double sd = 0.0;
   if (OP != FMX_CS_MEAN) {
-    double s2 = block_pw_sum<CS_NT>([&](int i) {
+    int c2;
+    const double s2 = block_pw_sum_w0<CSM_NT>([&](int i) {
       double t = v[i];
       double z = t == t ? t : 0.0;
       double q = (mean - z) * (mean - z);
       return t == t ? q : 0.0;
-    }, sch, nodes);
-    double var = cnt > 0 ? s2 / (double)cnt : qnan();
+    }, [](int) { return 0; }, sch, nodes, iscr, &c2);
+    const double var = cnt > 0 ? s2 / (double)cnt : qnan();
     sd = sqrt(var);
   }
-  (void)dscr;
+  if (stats && threadIdx.x == 0) { stats[2 * row] = mean; stats[2 * row + 1] = sd; }
+  if (OP == FMX_CS_STATS_ONLY) return;
   const bool guard = (OP == FMX_CS_MARKET_NEUTRALIZE) && (sd == 0.0 || sd != sd);
-  for (int i = threadIdx.x; i < n; i += CS_NT) {
+  for (int i = threadIdx.x; i < n; i += CSM_NT) {
     double t = v[i];
     double o;
     if (OP == FMX_CS_MEAN) o = mean;
@@ -89,7 +127,7 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
     y[a] = o;
   }
   if (prow) {
-    for (int64_t a = threadIdx.x; a < A; a += CS_NT)
+    for (int64_t a = threadIdx.x; a < A; a += CSM_NT)
       if (!prow[a]) y[a] = qnan();
   }
 }
@@ -458,11 +496,8 @@ static fmx_status set_lds(const void* k, size_t lds) {
 
 using namespace fmx;
 
-extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
-                                    int64_t ld, const uint8_t* present, void* stream) {
-  FMX_ARG(X && Y, "null panel");
-  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
-  FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_MARKET_NEUTRALIZE, "unknown cs op");
+static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                   const uint8_t* present, double* stats, void* stream) {
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   fmx_status e = FMX_OK;
   PwTable pw = pw_table((int)A, &e);
@@ -470,11 +505,30 @@ extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int6
   size_t lds = A * 8 + (present ? ((A * 2 + 15) & ~15) : 0) + (2 * (A / 64) + 8) * 8 + 16 * 4 + 64;
   const void* k = op == FMX_CS_ZSCORE ? (const void*)k_cs_moment<FMX_CS_ZSCORE>
                 : op == FMX_CS_MEAN ? (const void*)k_cs_moment<FMX_CS_MEAN>
-                                    : (const void*)k_cs_moment<FMX_CS_MARKET_NEUTRALIZE>;
+                : op == FMX_CS_MARKET_NEUTRALIZE ? (const void*)k_cs_moment<FMX_CS_MARKET_NEUTRALIZE>
+                                                 : (const void*)k_cs_moment<FMX_CS_STATS_ONLY>;
   if ((e = set_lds(k, lds))) return e;
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw};
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(CS_NT), args, lds, as_stream(stream)));
+  FMX_ARG(F * D <= 0x7fffffffll, "too many rows");
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(CSM_NT), args, lds, as_stream(stream)));
   return FMX_OK;
+}
+
+extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
+                                    int64_t ld, const uint8_t* present, void* stream) {
+  FMX_ARG(X && Y, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_MARKET_NEUTRALIZE, "unknown cs op");
+  return cs_moment_launch(op, X, Y, F, D, A, ld, present, nullptr, stream);
+}
+
+extern "C" fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
+                                          int64_t ld, const uint8_t* present, double* stats, void* stream) {
+  FMX_ARG(X && stats, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_STATS, "unknown cs op");
+  FMX_ARG(op == FMX_CS_STATS || Y, "null output panel");
+  return cs_moment_launch(op, X, op == FMX_CS_STATS ? nullptr : Y, F, D, A, ld, present, stats, stream);
 }
 
 extern "C" fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,

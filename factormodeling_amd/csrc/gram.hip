@@ -253,9 +253,203 @@ __global__ void k_gram_reduce(const double* __restrict__ part, int64_t nslice, i
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused Gram for F <= 256: one workgroup per K-slice (a date range) computes the whole
+// upper triangle of NB x NB 16x16 blocks (F padded to FP = 16 NB), reading the raw panel
+// once.  Per K chunk (32 assets of one date) the 1024 threads load FP x 32 exposures,
+// apply the z-score with the row stats (fmx_cs_moment_stats), and stage Z (fp64) and
+// M (bf16 0/1) in LDS; each wave then runs the fp64 16x16x4 MFMAs (8 k-steps) and one
+// bf16 16x16x32 MFMA of its triangle blocks (wave w owns triangle blocks w, w+16, ...).
+// The next chunk's loads are in flight during the MFMAs.
+constexpr int SG_NT = 1024;     // 16 waves: <= 6 triangle blocks per wave at F = 200
+constexpr int SG_K = 32;          // assets per K chunk
+constexpr int SG_KP = SG_K + 2;   // fp64 row pitch: conflict-free ds_read_b64 fragments
+constexpr int SG_MP = SG_K + 8;   // bf16 row pitch: 16-B aligned rows
+
+typedef float flt4 __attribute__((ext_vector_type(4)));
+
+template <int NB, int MODE>   // MODE 0: G = Z Z^T on fp64 MFMA; 1: N = M M^T on bf16 MFMA
+__global__ void __launch_bounds__(SG_NT)
+k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
+             int64_t ld, int64_t d0, int64_t d1, int64_t dps, double* __restrict__ part) {
+  constexpr int FP = 16 * NB;
+  constexpr int NTRI = NB * (NB + 1) / 2;
+  constexpr int NWV = SG_NT / 64;
+  constexpr int BPW = (NTRI + NWV - 1) / NWV;
+  constexpr int NEL = FP * SG_K;              // elements per chunk
+  constexpr int EPT = (NEL + SG_NT - 1) / SG_NT;   // loader elements per thread
+  __shared__ double Zs[MODE == 0 ? FP * SG_KP : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t Ms[MODE == 1 ? FP * SG_MP : 8];
+  __shared__ double mu_s[FP], sd_s[FP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t slice = blockIdx.x;
+  const int64_t ds = d0 + slice * dps;
+  const int64_t de = min<int64_t>(d1, ds + dps);
+  int blk[BPW];                                 // bi | bj << 8 (row-major triangle order), -1 = none
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) {
+    int j = wid + NWV * u, bi = 0;
+    blk[u] = -1;
+    if (j < NTRI) {
+      while (j >= NB - bi) { j -= NB - bi; ++bi; }
+      blk[u] = bi | ((bi + j) << 8);
+    }
+  }
+  dbl4 gacc[MODE == 0 ? BPW : 1];
+  flt4 nacc[MODE == 1 ? BPW : 1];
+#pragma unroll
+  for (int u = 0; u < (MODE == 0 ? BPW : 1); ++u) gacc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int u = 0; u < (MODE == 1 ? BPW : 1); ++u) nacc[u] = flt4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t nch = (A + SG_K - 1) / SG_K;
+  const int64_t total = (de - ds) * nch;
+  double xr[EPT];
+  auto issue = [&](int64_t c) {
+    const int64_t d = ds + c / nch, a0 = (c % nch) * SG_K;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
+      const int64_t a = a0 + cl;
+      xr[u] = (e < NEL && r < F && a < A) ? X[((int64_t)r * D + d) * ld + a] : qnan();
+    }
+  };
+  auto load_stats = [&](int64_t d) {
+    for (int r = tid; r < FP; r += SG_NT) {
+      mu_s[r] = r < F ? stats[2 * ((int64_t)r * D + d)] : 0.0;
+      sd_s[r] = r < F ? stats[2 * ((int64_t)r * D + d) + 1] : 0.0;
+    }
+  };
+  if (total > 0) {
+    issue(0);
+    load_stats(ds);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < total; ++c) {
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
+      if (e >= NEL) continue;
+      const double v = xr[u], sd = sd_s[r];
+      const bool ok = (v == v) && (sd > 0.0);
+      if (MODE == 0) Zs[r * SG_KP + cl] = ok ? (v - mu_s[r]) / sd : 0.0;
+      else Ms[r * SG_MP + cl] = ok ? (uint16_t)0x3f80 : (uint16_t)0;   // bf16 1.0 / 0.0
+    }
+    __syncthreads();
+    if (c + 1 < total) issue(c + 1);
+    if (MODE == 0) {
+#pragma unroll 1
+      for (int ks = 0; ks < SG_K; ks += 4) {     // not unrolled: bounds the fragment registers
+        const int kk = ks + (lane >> 4);
+#pragma unroll
+        for (int u = 0; u < BPW; ++u) {
+          if (blk[u] < 0) continue;               // wave-uniform
+          const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+          const double a = Zs[(bi * 16 + (lane & 15)) * SG_KP + kk];
+          const double b = Zs[(bj * 16 + (lane & 15)) * SG_KP + kk];
+          gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, gacc[u], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < BPW; ++u) {
+        if (blk[u] < 0) continue;
+        const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ms[(bi * 16 + (lane & 15)) * SG_MP + 8 * (lane >> 4)]);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Ms[(bj * 16 + (lane & 15)) * SG_MP + 8 * (lane >> 4)]);
+        nacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, nacc[u], 0, 0, 0);
+      }
+    }
+    // the stats of chunk c were consumed before the barrier above
+    if (c + 1 < total && (c + 1) % nch == 0) load_stats(ds + (c + 1) / nch);
+    __syncthreads();
+  }
+  double* p = part + slice * (int64_t)FP * FP;
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) {
+    if (blk[u] < 0) continue;
+    const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+    const int col = bj * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (MODE == 0) p[(bi * 16 + (lane >> 4) + 4 * r) * FP + col] = gacc[u][r];             // f64 16x16x4 C map
+      else p[(bi * 16 + 4 * (lane >> 4) + r) * FP + col] = (double)nacc[u & (MODE == 1 ? ~0 : 0)][r];  // bf16 16x16x32
+    }
+  }
+}
+
+// Sum the slices in order (deterministic) for the upper-triangle blocks and mirror.
+__global__ void k_gram_small_reduce(const double* __restrict__ partG, const double* __restrict__ partN,
+                                    int64_t nslice, int FP, int64_t F, double* __restrict__ G,
+                                    double* __restrict__ N, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)FP * FP) return;
+  const int i = (int)(e / FP), j = (int)(e % FP);
+  if ((i >> 4) > (j >> 4) || i >= F || j >= F) return;
+  const int64_t st = (int64_t)FP * FP;
+  double g = 0.0, n = 0.0;
+#pragma unroll 8
+  for (int64_t sl = 0; sl < nslice; ++sl) {
+    g += partG[sl * st + e];
+    n += partN[sl * st + e];
+  }
+  if (accumulate) {
+    g += G[(int64_t)i * F + j];
+    n += N[(int64_t)i * F + j];
+  }
+  G[(int64_t)i * F + j] = g;
+  G[(int64_t)j * F + i] = g;
+  N[(int64_t)i * F + j] = n;
+  N[(int64_t)j * F + i] = n;
+}
+
+template <int NB>
+static fmx_status gram_small_launch(const double* X, const double* stats, double* G, double* N, int64_t F,
+                                    int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int accumulate,
+                                    hipStream_t st) {
+  constexpr int FP = 16 * NB;
+  const int64_t ndates = d1 - d0;
+  int64_t nslice = std::min<int64_t>(ndates, 512);
+  const int64_t dps = ceil_div(ndates, nslice);
+  nslice = ceil_div(ndates, dps);
+  double* part = nullptr;
+  const int64_t st_elems = (int64_t)FP * FP * nslice;
+  FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * st_elems, st));
+  k_gram_small<NB, 0><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part);
+  FMX_LAUNCH_CHECK("k_gram_small<G>");
+  k_gram_small<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part + st_elems);
+  FMX_LAUNCH_CHECK("k_gram_small<N>");
+  k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(part, part + st_elems, nslice, FP,
+                                                                                  F, G, N, accumulate);
+  FMX_LAUNCH_CHECK("k_gram_small_reduce");
+  FMX_HIP(hipFreeAsync(part, st));
+  return FMX_OK;
+}
+
 }  // namespace fmx
 
 using namespace fmx;
+
+extern "C" fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F,
+                                     int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate,
+                                     void* stream) {
+  FMX_ARG(X && stats && G && N, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
+  if (F > 256) {
+    set_error("fmx_gram_fused supports F <= 256; use fmx_zscore_exposures + fmx_gram");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  if (F == 0 || d1 == d0) return FMX_OK;
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)ceil_div(F, 16);
+  switch (nb) {
+#define FMX_GS(K) \
+  case K: return gram_small_launch<K>(X, stats, G, N, F, D, A, ld, d0, d1, accumulate, st);
+    FMX_GS(1) FMX_GS(2) FMX_GS(3) FMX_GS(4) FMX_GS(5) FMX_GS(6) FMX_GS(7) FMX_GS(8)
+    FMX_GS(9) FMX_GS(10) FMX_GS(11) FMX_GS(12) FMX_GS(13) FMX_GS(14) FMX_GS(15) FMX_GS(16)
+#undef FMX_GS
+    default: return FMX_ERR_UNSUPPORTED;
+  }
+}
 
 extern "C" fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
                                            int64_t ld, void* stream) {

@@ -87,6 +87,79 @@ __device__ double block_pw_sum(Elem elem, const int32_t* __restrict__ sched, dou
   return r;
 }
 
+// block_pw_sum with a barrier-light combine: all threads form the 8-lane leaves (and
+// count the elements for which valid(i) holds), then wave 0 alone walks the combine
+// rounds (in-order LDS within one wave: no block barrier per round) and publishes the
+// root.  Returns the sum; *count receives the number of valid elements.
+// nodes: >= 2L+1 doubles; iscr: >= NT/64 + 1 ints.
+template <int NT, class Elem, class Valid>
+__device__ double block_pw_sum_w0(Elem elem, Valid valid, const int32_t* __restrict__ sched, double* nodes,
+                                  int* iscr, int* count) {
+  PwView s{sched};
+  const int L = s.L(), n = s.n();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int c = 0;
+  if (L == 0) {
+    for (int i = tid; i < n; i += NT) c += valid(i);
+  } else {
+    for (int t0 = 0; t0 < L * 8; t0 += NT) {
+      const int t = t0 + tid;
+      const bool act = t < L * 8;
+      const int leaf = t >> 3, j = t & 7;
+      double r = 0.0;
+      int st = 0, len = 0, stop = 0;
+      if (act) {                       // numpy leaves hold >= 8 elements
+        st = s.lstart(leaf);
+        len = s.llen(leaf);
+        stop = len - (len & 7);
+        r = elem(st + j);
+        c += valid(st + j);
+        for (int i = 8; i < stop; i += 8) { r += elem(st + i + j); c += valid(st + i + j); }
+      }
+      // ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) as an xor butterfly (IEEE + commutes)
+      r = r + __shfl_xor(r, 1);
+      r = r + __shfl_xor(r, 2);
+      r = r + __shfl_xor(r, 4);
+      if (act && j == 0) {
+        for (int i = stop; i < len; ++i) { r += elem(st + i); c += valid(st + i); }
+        nodes[leaf] = r;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) iscr[wid] = c;
+  __syncthreads();
+  if (wid == 0) {
+    if (L == 0) {
+      if (lane == 0) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += elem(i);
+        nodes[0] = r;
+      }
+    } else {
+      const int R = s.R();
+      const int32_t* tr = s.trip();
+      for (int rr = 0; rr < R; ++rr) {
+        for (int q = s.roff(rr) + lane; q < s.roff(rr + 1); q += 64)
+          nodes[tr[3 * q]] = nodes[tr[3 * q + 1]] + nodes[tr[3 * q + 2]];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // round r visible to round r+1
+      }
+      if (lane == 0) nodes[0] = nodes[s.root()];
+    }
+    if (lane == 0) {
+      int tot = 0;
+      for (int w = 0; w < NT / 64; ++w) tot += iscr[w];
+      iscr[NT / 64] = tot;
+    }
+  }
+  __syncthreads();
+  const double r = nodes[0];
+  *count = iscr[NT / 64];
+  __syncthreads();
+  return r;
+}
+
 // Exclusive scan of v across the block; *total receives the sum.  scratch: NT/64 ints.
 template <int NT>
 __device__ int block_exscan(int v, int* scratch, int* total) {

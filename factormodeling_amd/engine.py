@@ -104,6 +104,19 @@ def cs_moment(op: str, X, present=None, out=None):
     return Y
 
 
+def cs_moment_stats(op: str, X, present=None, out=None):
+    """fmx_cs_moment plus the per-row (mean, std ddof=0) [F][D][2]; op 'stats' returns
+    (None, stats) without writing an output panel."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Y = None if op == "stats" else _out(X, out)
+    stats = torch.empty((F, D, 2), dtype=F64, device=X.device)
+    call("fmx_cs_moment_stats", CS[op], ptr(X), ptr(Y), F, D, A, A, ptr(present), ptr(stats), stream_ptr())
+    return Y, stats
+
+
 def cs_rank(X, method="average", present=None, out=None):
     X = as3(X)
     _check_panel(X)
@@ -221,10 +234,35 @@ def gram(Z, M=None, d0=0, d1=None):
     return G, N
 
 
-def corr_matrix(X, d0=0, d1=None):
-    """Builder-defined factor correlation: C = G / N on fp64 MFMA."""
-    Z, M = zscore_exposures(X)
-    G, N = gram(Z, M, d0, d1)
+FUSED_GRAM_MAX_F = 256
+
+
+def gram_fused(X, stats, d0=0, d1=None):
+    """G, N straight from the raw panel with row stats (F <= 256): one pass over X."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous():
+        raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
+    d1 = D if d1 is None else d1
+    G = torch.empty((F, F), dtype=F64, device=X.device)
+    N = torch.empty((F, F), dtype=F64, device=X.device)
+    call("fmx_gram_fused", ptr(X), ptr(stats), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, stream_ptr())
+    return G, N
+
+
+def corr_matrix(X, d0=0, d1=None, stats=None):
+    """Builder-defined factor correlation: C = G / N on fp64 MFMA.  F <= 256
+    takes the fused path (row stats from cs_moment, one pass over X); wider panels
+    materialise Z/M and use the 128x128-tiled kernels."""
+    X = as3(X)
+    if X.shape[0] <= FUSED_GRAM_MAX_F:
+        if stats is None:
+            _, stats = cs_moment_stats("stats", X)
+        G, N = gram_fused(X, stats, d0, d1)
+    else:
+        Z, M = zscore_exposures(X)
+        G, N = gram(Z, M, d0, d1)
     return torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
 
 

@@ -132,6 +132,21 @@ class EngineBackend:
             return E.cs_quantile_op("winsor", X, 0.01, 0.99, out=out)
         raise ValueError(kind)
 
+    @staticmethod
+    def cs_zscore_stats(X, out):
+        """cs_zscore that also returns the per-row (mean, std) the Gram reuses."""
+        return E.cs_moment_stats("zscore", X, out=out)
+
+    @staticmethod
+    def corr_gram(X, d0, d1, stats=None):
+        """G, N over dates [d0, d1): fused single pass for F <= 256, else Z/M + tiles."""
+        if X.shape[0] <= E.FUSED_GRAM_MAX_F:
+            if stats is None:
+                _, stats = E.cs_moment_stats("stats", X)
+            return E.gram_fused(X, stats, d0, d1)
+        Z, M = E.zscore_exposures(X[:, d0:d1].contiguous())
+        return E.gram(Z, M)
+
     ic_daily = staticmethod(E.ic_daily)
     ic_window = staticmethod(E.ic_window)
     select_icir_top = staticmethod(E.select_icir_top)
@@ -143,13 +158,17 @@ class EngineBackend:
 ENGINE = EngineBackend()
 
 
-def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE, collect=None, own=slice(None)):
+def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None):
     """Operator set over the local panel (halo rows included as warm-up).  ``collect``
-    (a dict) receives a copy of every operator's owned-date output (tests only)."""
+    (a dict) receives a copy of every operator's owned-date output (tests only); ``side``
+    (a dict) receives by-products later stages reuse (cs_zscore's row stats)."""
     Y = out if out is not None else torch.empty_like(X)
     for kind, op, w in cfg.ops:
         t0 = _ev(timers)
-        be.op(kind, op, w, X, Y)
+        if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
+            _, side["stats"] = be.cs_zscore_stats(X, Y)
+        else:
+            be.op(kind, op, w, X, Y)
         _rec(timers, f"{kind}:{op or ''}:{w or ''}", t0)
         if collect is not None:
             collect[f"{kind}:{op or ''}:{w or ''}"] = Y[:, own].clone()
@@ -178,7 +197,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     t0 = _ev(timers)
     sp.exchange_halo()
     _rec(timers, "halo", t0)
-    run_ops(sp.X, cfg, timers=timers, be=be, collect=collect, own=slice(sp.halo, None))
+    side = {}
+    run_ops(sp.X, cfg, timers=timers, be=be, collect=collect, own=slice(sp.halo, None), side=side)
     # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     daily = be.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
@@ -204,9 +224,11 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     _rec(timers, "select", t0)
     # correlation Gram over owned dates, all-reduced
     t0 = _ev(timers)
-    Xo = sp.X[:, sp.halo:]
-    Z, M = be.zscore_exposures(Xo.contiguous())
-    G, N = be.gram(Z, M)
+    if hasattr(be, "corr_gram"):
+        G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
+    else:
+        Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
+        G, N = be.gram(Z, M)
     if sp.world > 1:
         dist.all_reduce(G)
         dist.all_reduce(N)

@@ -57,6 +57,7 @@ typedef int32_t fmx_status;
 #define FMX_CS_ZSCORE 0            /* operations.py:77  cs_zscore         */
 #define FMX_CS_MEAN 1              /* operations.py:85  cs_mean           */
 #define FMX_CS_MARKET_NEUTRALIZE 2 /* operations.py:171 market_neutralize */
+#define FMX_CS_STATS 3             /* row (mean, std ddof=0) only (fmx_cs_moment_stats) */
 
 /* rank methods (pandas Series.rank(method=...)) */
 #define FMX_RANK_AVERAGE 0
@@ -115,6 +116,11 @@ fmx_status fmx_ts_regression(const double* Yv, const double* Xv, const uint8_t* 
 /* ---- cross section (operations.py:54-101, 171-182, 248-304) ---------------------- */
 fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                          const uint8_t* present, void* stream);
+/* fmx_cs_moment that also writes stats[F][D][2] = (nanmean, nanstd ddof=0) per row, the
+ * numpy-pairwise moments cs_zscore uses (operations.py:77-78).  op FMX_CS_STATS writes
+ * only the stats (Y may be NULL); they feed fmx_gram_fused. */
+fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                               const uint8_t* present, double* stats, void* stream);
 /* cs_rank (operations.py:54-62): (rank - 1) / (rows - 1), rows counting NaN. */
 fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
                        const uint8_t* present, void* stream);
@@ -162,6 +168,12 @@ fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t
  * pair counts).  accumulate = 0 overwrites.  M/N may be NULL. */
 fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
                     int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
+/* Fused form for F <= 256: G and N straight from the raw panel X with the row stats of
+ * fmx_cs_moment_stats (z = (x - mean) / sd where x is non-NaN and sd > 0, else 0; M the
+ * same validity), one pass over X, both MFMA products in the same workgroup.  Returns
+ * FMX_ERR_UNSUPPORTED for F > 256 (use fmx_zscore_exposures + fmx_gram). */
+fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F, int64_t D,
+                          int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
 
 /* ---- composite factors (composite_factor.py:137-342) ------------------------------- */
 /* composite_factor_calculation preprocessing (:157-178): Adj[k] = suffix-scaled X[cols[k]]

@@ -230,3 +230,49 @@ def test_composite_vs_reference(fm):
         assert_close(out.to_numpy(), st[f"out_wcf_{meth}"], rtol=RTOL, atol=ATOL, what=f"wcf_{meth}")
     with pytest.raises(ValueError):
         cf.composite_factor_calculation(df, names, method="bogus")
+
+
+def test_cs_moment_stats_vs_oracle(fm):
+    """Row (mean, std ddof=0) by-product of cs_zscore == numpy pairwise nanmean/nanstd."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.numerics as nm
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((3, 17, 1000))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    X[1, 4] = np.nan                         # empty row -> NaN stats
+    X[2, 5] = 0.75                           # constant row -> sd 0
+    Y, st = E.cs_moment_stats("zscore", torch.as_tensor(X, device="cuda"))
+    st = st.cpu().numpy()
+    with np.errstate(all="ignore"):
+        mu, sd = nm.nanmean(X), nm.nanstd(X, 0)
+    assert_close(st[..., 0].ravel(), mu.ravel(), exact=True, what="mean")
+    assert_close(st[..., 1].ravel(), sd.ravel(), exact=True, what="sd")
+    _, st2 = E.cs_moment_stats("stats", torch.as_tensor(X, device="cuda"))
+    assert np.array_equal(st2.cpu().numpy(), st, equal_nan=True)
+
+
+def test_corr_gram_wide_vs_oracle(fm):
+    """F > 256 takes the materialised Z/M + 128x128-tile path."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(5)
+    F, D, A = 260, 3, 150
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    C = E.corr_matrix(torch.as_tensor(X, device="cuda")).cpu().numpy()
+    np.testing.assert_allclose(C, OG.corr_matrix(X), rtol=1e-10, atol=1e-12)
+
+
+def test_corr_gram_fused_date_range(fm):
+    """Fused Gram over a date sub-range [d0, d1) equals the oracle on that slice."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(6)
+    F, D, A = 37, 9, 401
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.1] = np.nan
+    C = E.corr_matrix(torch.as_tensor(X, device="cuda"), 2, 7).cpu().numpy()
+    np.testing.assert_allclose(C, OG.corr_matrix(X, 2, 7), rtol=1e-10, atol=1e-12)

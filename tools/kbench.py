@@ -65,6 +65,8 @@ OPS = {
     "winsor": (lambda X, R, Y: E.cs_quantile_op("winsor", X, 0.01, 0.99, out=Y), 16),
     "ic": (lambda X, R, Y: E.ic_daily(X, R, (1, 2)), 8),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
+    "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
+    "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
 }
 
 
