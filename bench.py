@@ -32,8 +32,41 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6           # MI355X fp64 (vector = matrix) spec
 
-# algorithmic bytes per factor·asset·day: unary op reads X once, writes once
-BYTES_PER_UNIT = {"ts": 16.0, "cs_rank": 16.0, "cs": 16.0, "winsor": 16.0}
+# algorithmic bytes per factor·asset·day: a unary operator reads X once and
+# writes once (16 B); the fused IC stage reads X once plus two R rows per (f, date) (8 + 16/F)
+def bytes_per_unit(stage, F):
+    kind = stage.split(":")[0]
+    if kind in ("ts", "cs_rank", "cs", "winsor"):
+        return 16.0
+    if kind == "ic_daily":
+        return 8.0 + 16.0 / F
+    return None
+
+
+# stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
+STAGE_KERNEL = {"ic_daily": "fmx::k_ic_daily_br<", "cs_rank": "fmx::k_cs_rank_br<",
+                "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",
+                "cs:market_neutralize": "fmx::k_cs_moment<2>", "ts:mean": "fmx::k_ts_reg<1,",
+                "ts:std": "fmx::k_ts_reg<2,", "ts:zscore": "fmx::k_ts_reg<4,", "ts:rank": "fmx::k_ts_reg<5,",
+                "ts:decay": "fmx::k_ts_reg<6,"}
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_c2.json")
+
+
+def pmc_traffic(stage, dims):
+    """HBM bytes per launch of the stage's kernel from the committed PMC summary (same
+    panel dims only), else None."""
+    try:
+        t = json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None
+    if list(t.get("dims", [])) != list(dims):
+        return None
+    key = ":".join(stage.split(":")[:2]).rstrip(":")
+    pre = STAGE_KERNEL.get(key)
+    for name, v in t.get("kernels", {}).items():
+        if pre and name.startswith(pre):
+            return v["traffic_bytes"]
+    return None
 
 
 def parse():
@@ -118,11 +151,13 @@ def main():
     units = float(D) * A * F
     value = units / (dt / args.steps)
 
-    # dominant kernel: the slowest operator stage (each is one kernel launch per step)
-    op_stages = {k: v / args.steps for k, v in stages.items() if k.split(":")[0] in BYTES_PER_UNIT}
+    # dominant kernel: the slowest HBM-priced stage (one launch of one kernel per step),
+    # timed with HIP events recorded on the launch stream inside the timed steps
+    op_stages = {k: v / args.steps for k, v in stages.items() if bytes_per_unit(k, F) is not None}
     dom, dom_ms = max(op_stages.items(), key=lambda kv: kv[1])
     local_units = float(F) * (sp.X.shape[1]) * A
-    achieved = BYTES_PER_UNIT[dom.split(":")[0]] * local_units / (dom_ms * 1e-3) / 1e9
+    achieved = bytes_per_unit(dom, F) * local_units / (dom_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(dom, [sp.X.shape[1], A, F]) if world == 1 else None
     if args.stages and rank == 0:
         for k, v in sorted(stages.items(), key=lambda kv: -kv[1]):
             print(f"stage {k:28s} {v / args.steps:9.3f} ms", file=sys.stderr)
@@ -149,7 +184,8 @@ def main():
             "config": {"workload": "C2 ops+IC+icir_top+corr-prune", "dates": D, "assets": A, "factors": F,
                        "parallelism": f"date-shard{world}", "sel_window": cfg.sel_window, "top_x": cfg.top_x},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes": bytes_per_unit(dom, F) * local_units, "ms": dom_ms},
             "stages_ms": {k: round(v / args.steps, 3) for k, v in stages.items()},
             "cpu_baseline": cpu,
         }

@@ -1,0 +1,5 @@
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OPS=ts_mean,ts_std,ts_zscore,ts_rank,ts_decay,cs_rank,cs_zscore,market_neutralize,winsor,ic,gram
+mkdir -p gpurun_out
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex fmx -f csv -d gpurun_out/pmcf_c2 -o run -- python tools/kbench.py --reps 1 --ops $OPS > gpurun_out/pmcf_c2.log 2>&1 && \
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex fmx -f csv -d gpurun_out/pmcw_c2 -o run -- python tools/kbench.py --reps 1 --ops $OPS > gpurun_out/pmcw_c2.log 2>&1 && echo pmc ok
