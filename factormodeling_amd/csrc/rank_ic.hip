@@ -1,5 +1,6 @@
 // Fused two-lag daily IC launcher (rank_kernels.hpp).
 // Reference: factor_selector.py:36-48
+#include "rank_fine.hpp"
 #include "rank_launch.hpp"
 
 namespace fmx {
@@ -23,7 +24,10 @@ __global__ void k_ic_empty(double* out, int64_t F, int64_t D, int L0, int L1, in
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                        const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
   const int nt = br_nt(1024);
-  const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8 + (size_t)((A + 15) & ~15ll);
+  const size_t lds_fr = (size_t)A * 8 + (size_t)((A + 15) & ~15ll);
+  auto fr_table = FMX_EMAX_TABLE(k_ic_daily_fr);
+  const bool fine = rank_impl() == RANK_IMPL_FINE && lds_fits(fr_table(nt, br_emax(A, nt)), lds_fr);
+  const size_t lds = fine ? lds_fr : (size_t)std::max<int64_t>(A, nt) * 8 + (size_t)((A + 15) & ~15ll);
   for (int base = 0; base < n_lags; base += 2) {
     int NL = std::min(2, n_lags - base);
     int L0 = lags_host[base], L1 = NL > 1 ? lags_host[base + 1] : 0;
@@ -32,7 +36,8 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
     FMX_LAUNCH_CHECK("k_ic_empty");
     void* args[] = {(void*)&X, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0, (void*)&L1,
                     (void*)&NL, (void*)&o};
-    fmx_status e = launch_br(FMX_EMAX_TABLE(k_ic_daily_br), nt, A, F * D, lds, args, st);
+    fmx_status e = fine ? launch_br(fr_table, nt, A, F * D, lds, args, st)
+                        : launch_br(FMX_EMAX_TABLE(k_ic_daily_br), nt, A, F * D, lds, args, st);
     if (e) return e;
   }
   return FMX_OK;

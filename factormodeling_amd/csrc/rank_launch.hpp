@@ -25,6 +25,25 @@ static inline int br_nt(int preferred) {
   return forced ? forced : preferred;
 }
 
+// Row-rank implementation: fine buckets (finerank.hpp, default) or splitter buckets
+// (bucketrank.hpp) with FMX_RANK_IMPL=br -- kept for A/B measurements.
+enum { RANK_IMPL_FINE = 0, RANK_IMPL_BR = 1 };
+static inline int rank_impl() {
+  static int v = [] {
+    const char* e = getenv("FMX_RANK_IMPL");
+    return (e && e[0] == 'b' && e[1] == 'r') ? (int)RANK_IMPL_BR : (int)RANK_IMPL_FINE;
+  }();
+  return v;
+}
+
+// True when kernel k (static LDS) plus dyn bytes of dynamic LDS fit one CU's 160 KiB.
+static inline bool lds_fits(const void* k, size_t dyn) {
+  if (!k) return false;
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, k) != hipSuccess) return false;
+  return at.sharedSizeBytes + dyn <= 160 * 1024;
+}
+
 template <class K>
 static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblocks, size_t lds, void** args,
                                    hipStream_t st) {
