@@ -28,10 +28,100 @@ namespace fmx {
 
 constexpr int FR_S = 64;   // samples = one wave
 
+// Lane index re-read at every call site: the persistent kernels loop over rows, and
+// without this the compiler hoists every shuffle's lane-derived address (and the bitonic
+// direction masks) out of the row loop into long-lived registers.
+__device__ __forceinline__ int fr_lane() {
+  int l = __lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ int fr_xor_i(int v, int m, int lane) {
+  return __builtin_amdgcn_ds_bpermute((lane ^ m) << 2, v);
+}
+__device__ __forceinline__ double fr_xor_d(double v, int m, int lane) {
+  const int a = (lane ^ m) << 2;
+  const uint64_t u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)u);
+  const int hi = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ uint64_t fr_xor_u64(uint64_t v, int m, int lane) {
+  const int a = (lane ^ m) << 2;
+  const int lo = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)v);
+  const int hi = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <class T>
+__device__ __forceinline__ T fr_up(T v, int o, int lane) {
+  const int a = (lane - o) << 2;            // lanes < o read garbage; callers mask them
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = (uint64_t)v;
+    const int lo = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)u);
+    const int hi = __builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(u >> 32));
+    return (T)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  } else {
+    return (T)__builtin_amdgcn_ds_bpermute(a, (int)v);
+  }
+}
+
+// 32-bit all-reduce over the 16 lanes of each DPP row (quad xor 1, xor 2, half-row
+// mirror, row mirror): every lane ends with its row's result.
+template <class Op>
+__device__ __forceinline__ uint32_t fr_row_allreduce(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  return v;
+}
+// Wave-uniform min / max / sum of a 32-bit value (row all-reduce + 4 lane reads).
+__device__ __forceinline__ uint32_t fr_wave_min_u32(uint32_t v) {
+  auto op = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
+  v = fr_row_allreduce(v, op);
+  return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+            op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint32_t fr_wave_max_u32(uint32_t v) {
+  auto op = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  v = fr_row_allreduce(v, op);
+  return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+            op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+// Value bounds from the high 32 bits of order keys: every key with high word in
+// [hmin, hmax] has a value in [lo, hi] (NaN patterns of the synthetic keys -> +-inf).
+__device__ __forceinline__ void fr_key_bounds(uint32_t hmin, uint32_t hmax, double* lo, double* hi) {
+  double a = okey_inv((uint64_t)hmin << 32), b = okey_inv(((uint64_t)hmax << 32) | 0xffffffffull);
+  *lo = (a == a) ? a : -INFINITY;
+  *hi = (b == b) ? b : INFINITY;
+}
+
+// Block reduction partials (as br_part, with fresh lane addresses): wave-reduce N values
+// (sum, or max when MAX) and park each wave's result at scr[wid*S + off + i].
+template <int N, bool MAX>
+__device__ __forceinline__ void fr_part(const double* v, double* scr, int S, int off) {
+  const int lane = fr_lane(), wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double x = v[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double y = fr_xor_d(x, o, lane);
+      x = MAX ? fmax(x, y) : x + y;
+    }
+    if (lane == 0) scr[wid * S + off + i] = x;
+  }
+}
+
 template <int K>
 struct FRG {
   static constexpr int NB = (FR_S + 1) * (K + 1) - 1;   // bucket ids [0, NB)
 };
+
+// fr_build_w0's sample argument meaning "the samples are parked in T.spl" (a key that
+// okey never produces: the NaN pattern's key sorts after +inf but before the sentinel).
+constexpr uint64_t FR_FROM_LDS = 0xfffffffffffffffeull;
 
 // LDS-resident cut of the key space.
 struct FrTab {
@@ -40,21 +130,15 @@ struct FrTab {
   double inv[FR_S + 1];      // K / (hi - lo), or 0 when the width is 0 / not finite
 };
 
-__device__ __forceinline__ uint64_t shfl_up1_u64(uint64_t v) {
-  const int lo = __shfl_up((int)(uint32_t)v, 1);
-  const int hi = __shfl_up((int)(uint32_t)(v >> 32), 1);
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
 
 // Ascending bitonic sort of one key per lane across a wave (lane l ends with the l-th
 // smallest); no LDS, no barrier.
-__device__ __forceinline__ uint64_t wave_sort64(uint64_t v) {
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t v, int lane) {
 #pragma unroll
   for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint64_t o = shfl_xor_u64(v, j);
+      const uint64_t o = fr_xor_u64(v, j, lane);
       const bool up = (lane & k) == 0;
       const bool lower = (lane & j) == 0;
       const uint64_t lo = v < o ? v : o, hi = v < o ? o : v;
@@ -74,9 +158,9 @@ __device__ __forceinline__ double fr_inv(double lo, double hi, double kf) {
 // vmin / vmax bound every key that will be bucketed (a superset's bounds are fine).
 template <int K>
 __device__ void fr_build_w0(FrTab& T, uint64_t sample_key, double vmin, double vmax) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t s = wave_sort64(sample_key);
-  const uint64_t prev = shfl_up1_u64(s);
+  const int lane = fr_lane();
+  const uint64_t s = wave_sort64(sample_key == FR_FROM_LDS ? T.spl[lane] : sample_key, lane);
+  const uint64_t prev = fr_up(s, 1, lane);
   const int ns = __popcll(__ballot(s != KEY_SENTINEL));
   T.spl[lane] = s;
   const double kf = (double)K;
@@ -115,10 +199,80 @@ __device__ __forceinline__ int fr_bucket(const FrTab& T, uint64_t key, double v)
   return i * (K + 1) + sub;
 }
 
+// Register sample: each of the NT/64 waves parks 64/(NT/64) of its keys in T.spl (lane j
+// of wave w gives its element k = (j + w) % EMAX, row position w*64 + j + k*NT), so the
+// 64 samples spread over every wave's columns and every register chunk at no memory
+// cost.  Wave 0 sorts them in place after the next barrier (fr_build_w0 with from_lds).
+template <int NT, int EMAX>
+__device__ __forceinline__ void fr_park_sample(FrTab& T, const uint64_t* key) {
+  constexpr int NW = NT / 64, PER = FR_S / NW;
+  const int lane = fr_lane(), wid = threadIdx.x >> 6;
+  if (lane < PER) {
+    const int sel = (lane + wid) % EMAX;
+    uint64_t v = KEY_SENTINEL;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (k == sel) v = key[k];
+    T.spl[wid * PER + lane] = v;
+  }
+}
+
+// Bucket ids of all EMAX keys of a thread, searched in lockstep (EMAX independent LDS
+// reads in flight per step) and branch-free; sentinel keys get bucket `dummy`.
+template <int K, int G>
+__device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* key, int* b, int dummy) {
+  int i[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) i[k] = 0;
+#pragma unroll
+  for (int step = 32; step >= 1; step >>= 1) {
+    uint64_t s[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) s[k] = T.spl[i[k] + step - 1];
+#pragma unroll
+    for (int k = 0; k < G; ++k) i[k] += (s[k] <= key[k]) ? step : 0;
+  }
+  {
+    uint64_t s[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) s[k] = T.spl[i[k]];
+#pragma unroll
+    for (int k = 0; k < G; ++k) i[k] += (s[k] <= key[k]) ? 1 : 0;   // #samples <= key
+  }
+  uint64_t sp[G];
+  double lo[G], inv[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    sp[k] = T.spl[i[k] > 0 ? i[k] - 1 : 0];   // i == 0: spl[0] > key, never equal
+    lo[k] = T.lo[i[k]];
+    inv[k] = T.inv[i[k]];
+  }
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const double tt = (okey_inv(key[k]) - lo[k]) * inv[k];
+    const int sub = inv[k] > 0.0 ? (int)fmin(tt, (double)(K - 1)) : 0;
+    const int be = (i[k] - 1) * (K + 1) + K, bf = i[k] * (K + 1) + sub;
+    b[k] = key[k] == KEY_SENTINEL ? dummy : (sp[k] == key[k] ? be : bf);
+  }
+}
+
+// Bucket ids of all EMAX keys of a thread, searched in lockstep groups of up to 5 (that
+// many independent LDS reads in flight per step) and branch-free; sentinel keys get
+// bucket `dummy`.
+template <int K, int EMAX>
+__device__ __forceinline__ void fr_bucket_all(const FrTab& T, const uint64_t* key, int* b, int dummy) {
+  if constexpr (EMAX <= 5) {
+    fr_bucket_grp<K, EMAX>(T, key, b, dummy);
+  } else {
+    fr_bucket_grp<K, 4>(T, key, b, dummy);
+    fr_bucket_all<K, EMAX - 4>(T, key + 4, b + 4, dummy);
+  }
+}
+
 // Positional sample of lane l: the element at the middle of the l-th of 64 equal strides
 // (NaN / absent -> sentinel).
 __device__ __forceinline__ uint64_t fr_sample(const double* x, const uint8_t* prow, int64_t A) {
-  const int lane = threadIdx.x & 63;
+  const int lane = fr_lane();
   const int64_t pos = ((int64_t)lane * A) / FR_S + A / (2 * FR_S);
   uint64_t sk = KEY_SENTINEL;
   if (pos < A && (prow ? prow[pos] != 0 : true)) {
@@ -133,7 +287,7 @@ __device__ __forceinline__ uint64_t fr_sample(const double* x, const uint8_t* pr
 template <int NT, class T>
 __device__ void fr_scan(T* c, int n, T* scr) {
   constexpr int NW = NT / 64;
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int t = threadIdx.x, lane = fr_lane(), wid = t >> 6;
   const int sc = (n + 1 + NT - 1) / NT;
   const int b0 = t * sc;
   T loc = 0;
@@ -142,7 +296,7 @@ __device__ void fr_scan(T* c, int n, T* scr) {
   T incl = loc;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const T u = __shfl_up(incl, o);
+    const T u = fr_up(incl, o, lane);
     if (lane >= o) incl += u;
   }
   if (lane == 63) scr[wid] = incl;

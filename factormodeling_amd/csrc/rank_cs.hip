@@ -1,22 +1,33 @@
-// cs_rank launcher: fine-bucket kernels (rank_fine.hpp) by default, the splitter-bucket
-// kernels (rank_kernels.hpp) with FMX_RANK_IMPL=br.
+// cs_rank launcher: persistent fine-bucket kernels (rank_fine.hpp) by default, the
+// splitter-bucket kernels (rank_kernels.hpp) with FMX_RANK_IMPL=br or when a row does not
+// fit the fine kernel's LDS.
 // Reference: operations.py:54-62
 #include "rank_fine.hpp"
 #include "rank_launch.hpp"
 
 namespace fmx {
 
+template <int NT, int E> constexpr auto kcr_dense = k_cs_rank_fa<NT, E, false>;
+template <int NT, int E> constexpr auto kcr_pres = k_cs_rank_fa<NT, E, true>;
+
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
                       const uint8_t* present, hipStream_t st) {
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
   const int nt = br_nt(1024);
-  const size_t lds_fr = (size_t)std::max<int64_t>(A, 1) * 8;
-  auto fr_table = FMX_EMAX_TABLE(k_cs_rank_fr);
-  if (rank_impl() == RANK_IMPL_BR || !lds_fits(fr_table(nt, br_emax(A, nt)), lds_fr)) {
+  const int nt_fa = fa_nt();
+  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)(FRG<FR_K_CS>::NB + 3) * 4);
+  const void* kfr = present ? FMX_EMAX_TABLE3(kcr_pres)(nt_fa, br_emax(A, nt_fa))
+                            : FMX_EMAX_TABLE3(kcr_dense)(nt_fa, br_emax(A, nt_fa));
+  if (rank_impl() == RANK_IMPL_BR || !lds_fits(kfr, lds_fr)) {
+    void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
     const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8;
     return launch_br(FMX_EMAX_TABLE(k_cs_rank_br), nt, A, F * D, lds, args, st);
   }
-  return launch_br(fr_table, nt, A, F * D, lds_fr, args, st);
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D == 0) return FMX_OK;
+  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
+  FMX_HIP(hipLaunchKernel(kfr, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  return FMX_OK;
 }
 
 }  // namespace fmx

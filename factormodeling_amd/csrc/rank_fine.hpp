@@ -14,131 +14,156 @@
 
 namespace fmx {
 
+// min waves per SIMD of the aliased-LDS cs_rank kernel: three rows per CU
+#ifndef FR_FA_WAVES
+#define FR_FA_WAVES(NT) ((NT) == 1024 ? 8 : ((NT) == 640 ? 8 : 6))
+#endif
+// Scheduling fence between unrolled per-element steps: bounds how many elements' live
+// ranges overlap (register pressure at 8 waves/SIMD) -- other waves hide the latency.
+#ifndef FR_NO_SCHED_FENCE
+#define FR_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define FR_SCHED_FENCE() (void)0
+#endif
 constexpr int FR_K_CS = 127;   // fine buckets per interval (cs_rank: 33 KB of int counters)
 constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows fit a CU)
 
 // ------------------------------------------------------------------------------------
 // cs_rank: y = (rank - 1) / (len(row) - 1), len counting NaN rows; 0.5 for single-row
 // dates (operations.py:58-60).  Rows are (f, d) = blockIdx.x / D, % D.
-template <int NT, int EMAX>
-__global__ void __launch_bounds__(NT)
-k_cs_rank_fr(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
+//
+// LDS is the occupancy limiter (rows in flight per CU hide each row's barrier and LDS
+// latency chain), so the bucket counters and the bucketed keys share one buffer: the
+// counters are read into registers after their scan, and only then are the keys of
+// shared fine buckets scattered over them.  ~42 KB per row: three rows per CU.
+// Positions t + k*NT with k < EMAX-1 are always inside the row (EMAX = ceil(A/NT)).
+template <int NT, int EMAX, bool PRES>
+__global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
+k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present) {
   constexpr int K = FR_K_CS, NB = FRG<K>::NB, NW = NT / 64;
   __shared__ FrTab tab;
-  __shared__ int cnt[NB + 1];
-  __shared__ double dscr[(NW + 1) * 4];
+  __shared__ uint4 wred[NW];                  // per wave: #present, #valid, min / max key high words
   __shared__ int iscr[NW];
-  extern __shared__ uint64_t bkey[];          // A keys
+  extern __shared__ uint64_t lds[];           // max(A keys, NB + 3 counters)
+  int* cnt = (int*)lds;                       // [NB] = total, [NB+1] = sentinel dummy
+  uint64_t* bkey = lds;
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
   const int64_t row = blockIdx.x;
-  const int64_t d = row % D;
   const double* x = X + row * ld;
   double* y = Y + row * ld;
-  const uint8_t* prow = present ? present + d * ld : nullptr;
+  const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
+  const int An = (int)A;
+  const bool last_in = t + (EMAX - 1) * NT < An;
   uint64_t key[EMAX];
-  double st[4] = {0.0, 0.0, -INFINITY, -INFINITY};   // nrow, nvalid, -min, max
+  uint32_t pm = 0, hmin = 0xffffffffu, hmax = 0u;
+  int wv = 0, wp = 0;                         // wave-uniform counts (ballots)
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const int64_t i = t + (int64_t)k * NT;
-    key[k] = KEY_SENTINEL;
-    if (i < A) {
-      const bool p = prow ? prow[i] != 0 : true;
-      const double v = x[i];
-      st[0] += p;
-      if (p && v == v) {
-        key[k] = okey(v);
-        st[1] += 1.0;
-        st[2] = fmax(st[2], -v);
-        st[3] = fmax(st[3], v);
-      }
-    }
+    const bool in = k < EMAX - 1 || last_in;
+    const double v = in ? x[t + k * NT] : 0.0;
+    const bool p = in && (PRES ? prow[t + k * NT] != 0 : true);
+    const bool ok = p && v == v;
+    pm |= (uint32_t)p << k;
+    key[k] = ok ? okey(v) : KEY_SENTINEL;
+    const uint32_t h = (uint32_t)(key[k] >> 32);
+    hmin = ok ? min(hmin, h) : hmin;
+    hmax = ok ? max(hmax, h) : hmax;
+    wv += __popcll(__ballot(ok));
+    if (PRES) wp += __popcll(__ballot(p));
   }
-  const uint64_t smp = wid == 0 ? fr_sample(x, prow, A) : KEY_SENTINEL;
-  for (int b = t; b <= NB; b += NT) cnt[b] = 0;
-  br_part<2, false>(st, dscr, 4, 0);
-  br_part<2, true>(st + 2, dscr, 4, 2);
-  br_fin<NT>(dscr, 4, 2);
-  const int nrow = (int)dscr[NW * 4 + 0], nv = (int)dscr[NW * 4 + 1];
-  const double vmin = -dscr[NW * 4 + 2], vmax = dscr[NW * 4 + 3];
-  BR_PH();
-  if (method == FMX_RANK_AVERAGE_PROPAGATE && nv < nrow) {
-#pragma unroll
-    for (int k = 0; k < EMAX; ++k) {
-      const int64_t i = t + (int64_t)k * NT;
-      if (i < A) y[i] = qnan();
-    }
-    return;
+  fr_park_sample<NT, EMAX>(tab, key);
+  for (int b = t; b < NB + 3; b += NT) cnt[b] = 0;
+  {
+    const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
+    if ((t & 63) == 0) wred[wid] = make_uint4((uint32_t)wp, (uint32_t)wv, a, c);
   }
-  const bool half = (method != FMX_RANK_AVERAGE_PROPAGATE) && nrow == 1;
-  if (half || nv == 0) {
-#pragma unroll
-    for (int k = 0; k < EMAX; ++k) {
-      const int64_t i = t + (int64_t)k * NT;
-      if (i < A) {
-        const bool p = prow ? prow[i] != 0 : true;
-        y[i] = (p && half) ? 0.5 : qnan();
-      }
-    }
-    return;
-  }
-  if (wid == 0) fr_build_w0<K>(tab, smp, vmin, vmax);
   __syncthreads();
   BR_PH();
-  int pk[EMAX];                               // slot | bucket << PK_BSHIFT
+  int nrow = An, nv = 0;
+  uint32_t h0 = 0xffffffffu, h1 = 0u;
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) {
-    if (key[k] != KEY_SENTINEL) {
-      const int b = fr_bucket<K>(tab, key[k], okey_inv(key[k]));
-      pk[k] = atomicAdd(&cnt[b], 1) | (b << PK_BSHIFT);
-    }
+  for (int w = 0; w < NW; ++w) {
+    const uint4 r = wred[w];
+    if (PRES) nrow = (w == 0 ? 0 : nrow) + (int)r.x;
+    nv += (int)r.y;
+    h0 = min(h0, r.z);
+    h1 = max(h1, r.w);
+  }
+  if ((method == FMX_RANK_AVERAGE_PROPAGATE && nv < nrow) || nv == 0 ||
+      (method != FMX_RANK_AVERAGE_PROPAGATE && nrow == 1)) {
+    // scipy propagate: one NaN -> all NaN; single-row date -> 0.5 (operations.py:58)
+    const bool half = (method != FMX_RANK_AVERAGE_PROPAGATE) && nrow == 1;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+    return;
+  }
+  if (wid == 0) {
+    double vmin, vmax;
+    fr_key_bounds(h0, h1, &vmin, &vmax);
+    fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
+  }
+  __syncthreads();
+  BR_PH();
+  int sl[EMAX];                               // slot | bucket << PK_BSHIFT, then start | len << 16
+  {
+    int bb[EMAX];
+    fr_bucket_all<K, EMAX>(tab, key, bb, NB + 1);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) sl[k] = atomicAdd(&cnt[bb[k]], 1) | (bb[k] << PK_BSHIFT);
   }
   __syncthreads();
   fr_scan<NT, int>(cnt, NB, iscr);
   BR_PH();
-  // le[k] = #less | #equal << 16 inside the bucket; only shared fine buckets need the scan
-  int s0[EMAX], len[EMAX], le[EMAX];
+  // le[k] = #less | #equal << 16 inside the bucket (for elements still to scan: their
+  // scatter slot until the scatter is done)
+  int le[EMAX];
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int b = sl[k] >> PK_BSHIFT;
+    const int slot = sl[k] & PK_SLOT;
+    const int s0 = cnt[b];
+    const int n = cnt[b + 1] - s0;
+    const bool eqb = (b % (K + 1)) == K;      // equal-to-sample bucket: all members tie
+    const bool scan = !eqb && n > 1 && b <= NB;
+    le[k] = scan ? slot : (eqb ? n : 1) << 16;
+    sl[k] = s0 | (scan ? n << 16 : 0);
+  }
+  __syncthreads();                            // counters dead: the keys reuse their LDS
   int maxlen = 0;
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    s0[k] = 0; len[k] = 0; le[k] = 0;
-    if (key[k] == KEY_SENTINEL) continue;
-    const int b = pk[k] >> PK_BSHIFT;
-    s0[k] = cnt[b];
-    const int n = cnt[b + 1] - s0[k];
-    if ((b % (K + 1)) == K) le[k] = n << 16;           // equal-to-sample bucket
-    else if (n == 1) le[k] = 1 << 16;
-    else {
-      len[k] = n;
-      bkey[s0[k] + (pk[k] & PK_SLOT)] = key[k];
+    const int n = sl[k] >> 16;
+    if (n) {
+      bkey[(sl[k] & 0xffff) + le[k]] = key[k];
+      le[k] = 0;
     }
-    maxlen = max(maxlen, len[k]);
+    maxlen = max(maxlen, n);
   }
   __syncthreads();
   BR_PH();
   for (int j = 0; j < maxlen; ++j) {
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      if (j < len[k]) {
-        const uint64_t w = bkey[s0[k] + j];
-        le[k] += (w < key[k]) + ((w == key[k]) << 16);
+      if (j < (sl[k] >> 16)) {                // exec-masked: idle lanes cost no LDS
+        const uint64_t w = bkey[(sl[k] & 0xffff) + j];
+        le[k] += (w < key[k] ? 1 : 0) + (w == key[k] ? 0x10000 : 0);
       }
     }
   }
   const double den = (double)(nrow - 1);
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const int64_t i = t + (int64_t)k * NT;
-    if (i >= A) continue;
-    if (key[k] == KEY_SENTINEL) { y[i] = qnan(); continue; }
+    if (!(k < EMAX - 1 || last_in)) continue;
     const int lt = le[k] & 0xffff, eq = le[k] >> 16;
-    const int less = s0[k] + lt;
+    const int less = (sl[k] & 0xffff) + lt;
     double r;
     if (method == FMX_RANK_MIN) r = (double)(less + 1);
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
-    y[i] = (r - 1.0) / den;
+    y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
   }
   BR_PH();
 }

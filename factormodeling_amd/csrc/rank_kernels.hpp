@@ -26,6 +26,7 @@ static __device__ unsigned long long br_phase_acc[32];
     }                                                                                  \
     ++br_ph_i;                                                                         \
   } while (0)
+#define BR_PH_ROW() br_ph_i = 0
 #define BR_PHASE_EXPORT(NAME)                                                          \
   extern "C" int NAME(unsigned long long* out) {                                       \
     unsigned long long z[32] = {};                                                     \
@@ -35,6 +36,7 @@ static __device__ unsigned long long br_phase_acc[32];
 #else
 #define BR_PH_INIT (void)0
 #define BR_PH() (void)0
+#define BR_PH_ROW() (void)0
 #define BR_PHASE_EXPORT(NAME)
 #endif
 

@@ -2,6 +2,8 @@
 // rank_q.hip, rank_ic.hip): row-length -> EMAX table, workgroup size choice.
 #pragma once
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include "rank_kernels.hpp"
 
 namespace fmx {
@@ -56,6 +58,33 @@ static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblo
   return FMX_OK;
 }
 
+// Launch of a persistent row kernel: as many workgroups as are co-resident on the
+// device (occupancy x CUs), capped at the row count; the kernel walks the rows.
+static inline fmx_status launch_persistent(const void* k, int nt, int64_t nrows, size_t lds, void** args,
+                                           hipStream_t st) {
+  if (!k) { set_error("row too long for the fine-bucket kernels"); return FMX_ERR_UNSUPPORTED; }
+  if (nrows <= 0) return FMX_OK;
+  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int64_t> cache;
+  int64_t slots;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({k, lds});
+    if (it == cache.end()) {
+      int dev = 0, cus = 0, per = 0;
+      FMX_HIP(hipGetDevice(&dev));
+      FMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      FMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, nt, lds));
+      it = cache.emplace(std::make_pair(k, lds), (int64_t)std::max(1, per) * std::max(1, cus)).first;
+    }
+    slots = it->second;
+  }
+  const int64_t grid = std::min<int64_t>(nrows, slots);
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)grid), dim3(nt), args, lds, st));
+  return FMX_OK;
+}
+
 #define FMX_EMAX_CASES(KT, NT)                                               \
   switch (E) {                                                               \
     case 1: return (const void*)KT<NT, 1>;                                   \
@@ -72,6 +101,23 @@ static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblo
     case 24: return (const void*)KT<NT, 24>;                                 \
     case 32: return (const void*)KT<NT, 32>;                                 \
     default: return (const void*)nullptr;                                    \
+  }
+
+// Workgroup size of the aliased-LDS cs_rank kernel (FMX_FA_NT=512|640|1024).
+static inline int fa_nt() {
+  static int v = [] {
+    const char* e = getenv("FMX_FA_NT");
+    const int x = e ? atoi(e) : 0;
+    return (x == 512 || x == 640 || x == 1024) ? x : 512;
+  }();
+  return v;
+}
+
+#define FMX_EMAX_TABLE3(KT)                                                  \
+  [](int nt, int E) -> const void* {                                         \
+    if (nt == 512) { FMX_EMAX_CASES(KT, 512) }                               \
+    if (nt == 640) { FMX_EMAX_CASES(KT, 640) }                               \
+    FMX_EMAX_CASES(KT, 1024)                                                 \
   }
 
 #define FMX_EMAX_TABLE(KT)                                                   \
