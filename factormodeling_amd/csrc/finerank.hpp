@@ -126,8 +126,8 @@ constexpr uint64_t FR_FROM_LDS = 0xfffffffffffffffeull;
 // LDS-resident cut of the key space.
 struct FrTab {
   uint64_t spl[FR_S];        // sorted sample keys, KEY_SENTINEL-padded
-  double lo[FR_S + 1];       // interval lower bound (value)
-  double inv[FR_S + 1];      // K / (hi - lo), or 0 when the width is 0 / not finite
+  double2 li[FR_S + 1];      // interval (lower bound, K / (hi - lo) or 0 when the width
+                             // is 0 / not finite): one 16-byte read per element
 };
 
 
@@ -170,16 +170,14 @@ __device__ void fr_build_w0(FrTab& T, uint64_t sample_key, double vmin, double v
     const double hi = lane == ns ? vmax : okey_inv(s);
     inv = fr_inv(lo, hi, kf);
   }
-  T.lo[lane] = lo;
-  T.inv[lane] = inv;
+  T.li[lane] = make_double2(lo, inv);
   if (lane == 63) {                       // interval 64 exists only when ns == 64
     double lo64 = 0.0, inv64 = 0.0;
     if (ns == 64) {
       lo64 = okey_inv(s);
       inv64 = fr_inv(lo64, vmax, kf);
     }
-    T.lo[64] = lo64;
-    T.inv[64] = inv64;
+    T.li[64] = make_double2(lo64, inv64);
   }
 }
 
@@ -193,8 +191,9 @@ __device__ __forceinline__ int fr_bucket(const FrTab& T, uint64_t key, double v)
   const uint64_t last = T.spl[i];
   i += last <= key;                         // i = #samples <= key, in [0, 64]
   if (i > 0 && T.spl[i - 1] == key) return (i - 1) * (K + 1) + K;
-  const double inv = T.inv[i];
-  const double t = (v - T.lo[i]) * inv;
+  const double2 li = T.li[i];
+  const double inv = li.y;
+  const double t = (v - li.x) * inv;
   const int sub = inv > 0.0 ? (int)fmin(t, (double)(K - 1)) : 0;
   return i * (K + 1) + sub;
 }
@@ -217,11 +216,10 @@ __device__ __forceinline__ void fr_park_sample(FrTab& T, const uint64_t* key) {
   }
 }
 
-// Bucket ids of all EMAX keys of a thread, searched in lockstep (EMAX independent LDS
-// reads in flight per step) and branch-free; sentinel keys get bucket `dummy`.
 template <int K, int G>
 __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* key, int* b, int dummy) {
   int i[G];
+  uint64_t last[G];                           // largest sample <= key
 #pragma unroll
   for (int k = 0; k < G; ++k) i[k] = 0;
 #pragma unroll
@@ -230,29 +228,33 @@ __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* ke
 #pragma unroll
     for (int k = 0; k < G; ++k) s[k] = T.spl[i[k] + step - 1];
 #pragma unroll
-    for (int k = 0; k < G; ++k) i[k] += (s[k] <= key[k]) ? step : 0;
+    for (int k = 0; k < G; ++k) {
+      const bool c = s[k] <= key[k];
+      i[k] += c ? step : 0;
+    }
   }
   {
     uint64_t s[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) s[k] = T.spl[i[k]];
 #pragma unroll
-    for (int k = 0; k < G; ++k) i[k] += (s[k] <= key[k]) ? 1 : 0;   // #samples <= key
+    for (int k = 0; k < G; ++k) {
+      const bool c = s[k] <= key[k];
+      i[k] += c ? 1 : 0;                      // #samples <= key
+    }
   }
-  uint64_t sp[G];
-  double lo[G], inv[G];
+  double2 li[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) li[k] = T.li[i[k]];
+#pragma unroll
+  for (int k = 0; k < G; ++k) last[k] = T.spl[i[k] > 0 ? i[k] - 1 : 0];   // i == 0: never equal
 #pragma unroll
   for (int k = 0; k < G; ++k) {
-    sp[k] = T.spl[i[k] > 0 ? i[k] - 1 : 0];   // i == 0: spl[0] > key, never equal
-    lo[k] = T.lo[i[k]];
-    inv[k] = T.inv[i[k]];
-  }
-#pragma unroll
-  for (int k = 0; k < G; ++k) {
-    const double tt = (okey_inv(key[k]) - lo[k]) * inv[k];
-    const int sub = inv[k] > 0.0 ? (int)fmin(tt, (double)(K - 1)) : 0;
+    const double tt = (okey_inv(key[k]) - li[k].x) * li[k].y;
+    const int sub = li[k].y > 0.0 ? (int)fmin(tt, (double)(K - 1)) : 0;
     const int be = (i[k] - 1) * (K + 1) + K, bf = i[k] * (K + 1) + sub;
-    b[k] = key[k] == KEY_SENTINEL ? dummy : (sp[k] == key[k] ? be : bf);
+    // a sentinel key (> every real key) only matches sentinel padding: dummy either way
+    b[k] = key[k] == KEY_SENTINEL ? dummy : (last[k] == key[k] ? be : bf);
   }
 }
 
@@ -280,6 +282,60 @@ __device__ __forceinline__ uint64_t fr_sample(const double* x, const uint8_t* pr
     if (v == v) sk = okey(v);
   }
   return sk;
+}
+
+// Packed 16-bit bucket counters: bucket b lives in half (b & 1) of word b >> 1.
+__device__ __forceinline__ uint32_t fr_cnt_add(uint32_t* w, int b) {
+  const uint32_t sh = (b & 1) << 4;
+  return (atomicAdd(&w[b >> 1], 1u << sh) >> sh) & 0xffffu;
+}
+__device__ __forceinline__ uint32_t fr_cnt_get(const uint32_t* w, int b) {
+  return (w[b >> 1] >> ((b & 1) << 4)) & 0xffffu;
+}
+
+// In-place exclusive scan of WORDS packed 16-bit counters (2 per word, 16-byte aligned),
+// every thread owning a run of WORDS/NT consecutive words read and written as uint4.
+// Exclusive starts stay below 65536 as long as the counted total (plus whatever sits in
+// the last half-word) does.  scr: NT/64 ints.  Every thread must call it.
+template <int NT, int WORDS>
+__device__ void fr_scan16(uint32_t* w, int* scr) {
+  constexpr int NW = NT / 64, R = WORDS / NT;
+  static_assert(WORDS % (4 * NT) == 0, "run of whole uint4s");
+  const int t = threadIdx.x, lane = fr_lane(), wid = t >> 6;
+  uint4* v = reinterpret_cast<uint4*>(w) + t * (R / 4);
+  auto sum4 = [](uint4 q) {
+    return (int)((q.x & 0xffffu) + (q.x >> 16) + (q.y & 0xffffu) + (q.y >> 16) + (q.z & 0xffffu) + (q.z >> 16) +
+                 (q.w & 0xffffu) + (q.w >> 16));
+  };
+  int loc = 0;
+#pragma unroll
+  for (int j = 0; j < R / 4; ++j) loc += sum4(v[j]);
+  int incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = fr_up(incl, o, lane);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) scr[wid] = incl;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) base += (x < wid) ? scr[x] : 0;
+  uint32_t run = (uint32_t)(base + incl - loc);
+  auto ex = [&](uint32_t word) {
+    const uint32_t lo = run, c0 = word & 0xffffu;
+    const uint32_t hi = run + c0;
+    run = hi + (word >> 16);
+    return (lo & 0xffffu) | (hi << 16);
+  };
+#pragma unroll
+  for (int j = 0; j < R / 4; ++j) {      // re-read: the run is not held in registers
+    const uint4 q = v[j];
+    uint4 o;
+    o.x = ex(q.x); o.y = ex(q.y); o.z = ex(q.z); o.w = ex(q.w);
+    v[j] = o;
+  }
+  __syncthreads();
 }
 
 // In-place exclusive scan of c[0..n) with c[n] = total, by a block of NT threads (each

@@ -13,10 +13,10 @@ template <int NT, int E> constexpr auto kcr_pres = k_cs_rank_fa<NT, E, true>;
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
                       const uint8_t* present, hipStream_t st) {
   const int nt = br_nt(1024);
-  const int nt_fa = fa_nt();
-  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)(FRG<FR_K_CS>::NB + 3) * 4);
-  const void* kfr = present ? FMX_EMAX_TABLE3(kcr_pres)(nt_fa, br_emax(A, nt_fa))
-                            : FMX_EMAX_TABLE3(kcr_dense)(nt_fa, br_emax(A, nt_fa));
+  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
+  const void* kfr = present ? FMX_EMAX_TABLE(kcr_pres)(nt_fa, br_emax(A, nt_fa))
+                            : FMX_EMAX_TABLE(kcr_dense)(nt_fa, br_emax(A, nt_fa));
   if (rank_impl() == RANK_IMPL_BR || !lds_fits(kfr, lds_fr)) {
     void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
     const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8;

@@ -25,7 +25,8 @@ namespace fmx {
 #else
 #define FR_SCHED_FENCE() (void)0
 #endif
-constexpr int FR_K_CS = 127;   // fine buckets per interval (cs_rank: 33 KB of int counters)
+constexpr int FR_K_CS = 247;   // fine buckets per interval (cs_rank: 16-bit counters, 32 KB)
+constexpr int FR_CS_WORDS = 8192;
 constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows fit a CU)
 
 // ------------------------------------------------------------------------------------
@@ -41,12 +42,14 @@ template <int NT, int EMAX, bool PRES>
 __global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present) {
-  constexpr int K = FR_K_CS, NB = FRG<K>::NB, NW = NT / 64;
+  constexpr int K = FR_K_CS, NW = NT / 64;
+  constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
+  static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
   __shared__ FrTab tab;
   __shared__ uint4 wred[NW];                  // per wave: #present, #valid, min / max key high words
   __shared__ int iscr[NW];
-  extern __shared__ uint64_t lds[];           // max(A keys, NB + 3 counters)
-  int* cnt = (int*)lds;                       // [NB] = total, [NB+1] = sentinel dummy
+  extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters)
+  uint32_t* cnt = (uint32_t*)lds;             // 16-bit counter of bucket b: half b & 1 of word b >> 1
   uint64_t* bkey = lds;
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
@@ -74,7 +77,9 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (PRES) wp += __popcll(__ballot(p));
   }
   fr_park_sample<NT, EMAX>(tab, key);
-  for (int b = t; b < NB + 3; b += NT) cnt[b] = 0;
+#pragma unroll
+  for (int j = 0; j < WORDS / (4 * NT); ++j)
+    reinterpret_cast<uint4*>(cnt)[t * (WORDS / (4 * NT)) + j] = make_uint4(0u, 0u, 0u, 0u);
   {
     const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
     if ((t & 63) == 0) wred[wid] = make_uint4((uint32_t)wp, (uint32_t)wv, a, c);
@@ -110,12 +115,12 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   int sl[EMAX];                               // slot | bucket << PK_BSHIFT, then start | len << 16
   {
     int bb[EMAX];
-    fr_bucket_all<K, EMAX>(tab, key, bb, NB + 1);
+    fr_bucket_all<K, EMAX>(tab, key, bb, DUMMY);
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) sl[k] = atomicAdd(&cnt[bb[k]], 1) | (bb[k] << PK_BSHIFT);
+    for (int k = 0; k < EMAX; ++k) sl[k] = (int)fr_cnt_add(cnt, bb[k]) | (bb[k] << PK_BSHIFT);
   }
   __syncthreads();
-  fr_scan<NT, int>(cnt, NB, iscr);
+  fr_scan16<NT, WORDS>(cnt, iscr);
   BR_PH();
   // le[k] = #less | #equal << 16 inside the bucket (for elements still to scan: their
   // scatter slot until the scatter is done)
@@ -124,10 +129,10 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   for (int k = 0; k < EMAX; ++k) {
     const int b = sl[k] >> PK_BSHIFT;
     const int slot = sl[k] & PK_SLOT;
-    const int s0 = cnt[b];
-    const int n = cnt[b + 1] - s0;
+    const int s0 = (int)fr_cnt_get(cnt, b);
+    const int n = (int)fr_cnt_get(cnt, b + 1) - s0;
     const bool eqb = (b % (K + 1)) == K;      // equal-to-sample bucket: all members tie
-    const bool scan = !eqb && n > 1 && b <= NB;
+    const bool scan = !eqb && n > 1 && b != DUMMY;
     le[k] = scan ? slot : (eqb ? n : 1) << 16;
     sl[k] = s0 | (scan ? n << 16 : 0);
   }
