@@ -89,6 +89,79 @@ __device__ __forceinline__ uint32_t fr_wave_max_u32(uint32_t v) {
             op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
+// f64 DPP moves (two 32-bit halves) and wave sums: row all-reduce by quad xor 1, xor 2,
+// half-row mirror, row mirror, then the four row totals through lane reads.  The
+// summation order is fixed, so results are run-to-run deterministic.
+template <int CTRL>
+__device__ __forceinline__ double fr_dpp_d(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double fr_row_sum_d(double v) {
+  v += fr_dpp_d<0xB1>(v);
+  v += fr_dpp_d<0x4E>(v);
+  v += fr_dpp_d<0x141>(v);
+  v += fr_dpp_d<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ double fr_readlane_d(double v, int l) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double fr_wave_sum_d(double v) {
+  v = fr_row_sum_d(v);
+  return (fr_readlane_d(v, 0) + fr_readlane_d(v, 16)) + (fr_readlane_d(v, 32) + fr_readlane_d(v, 48));
+}
+__device__ __forceinline__ uint64_t fr_readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double fr_dpp_max_step(double v) {
+  return fmax(v, fr_dpp_d<CTRL>(v));
+}
+// Block reduction without LDS shuffles (as br_part / br_fin): every wave reduces N values
+// with DPP row all-reduces plus four lane reads, lane 0 parks them at scr[wid*S + off + i];
+// fr_fin_dpp then combines the NT/64 wave results of value i < S (sum for i < nsum, max
+// otherwise) into scr[(NT/64)*S + i].  scr: (NT/64 + 1) * S doubles.
+template <int N, bool MAX>
+__device__ __forceinline__ void fr_part_dpp(const double* v, double* scr, int S, int off) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double x = v[i];
+    if (MAX) {
+      x = fr_dpp_max_step<0xB1>(x);
+      x = fr_dpp_max_step<0x4E>(x);
+      x = fr_dpp_max_step<0x141>(x);
+      x = fr_dpp_max_step<0x140>(x);
+      x = fmax(fmax(fr_readlane_d(x, 0), fr_readlane_d(x, 16)), fmax(fr_readlane_d(x, 32), fr_readlane_d(x, 48)));
+    } else {
+      x = fr_row_sum_d(x);
+      x = (fr_readlane_d(x, 0) + fr_readlane_d(x, 16)) + (fr_readlane_d(x, 32) + fr_readlane_d(x, 48));
+    }
+    if (lane == 0) scr[wid * S + off + i] = x;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void fr_fin_dpp(double* scr, int S, int nsum) {
+  constexpr int NR = NT / 64;
+  const int t = threadIdx.x;
+  __syncthreads();
+  if (t < S) {
+    double x = scr[t];
+    for (int w = 1; w < NR; ++w) x = (t < nsum) ? x + scr[w * S + t] : fmax(x, scr[w * S + t]);
+    scr[NR * S + t] = x;
+  }
+  __syncthreads();
+}
+
 // Value bounds from the high 32 bits of order keys: every key with high word in
 // [hmin, hmax] has a value in [lo, hi] (NaN patterns of the synthetic keys -> +-inf).
 __device__ __forceinline__ void fr_key_bounds(uint32_t hmin, uint32_t hmax, double* lo, double* hi) {

@@ -244,9 +244,9 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   }
   const uint64_t smp = wid == 0 ? fr_sample(xf, nullptr, A) : KEY_SENTINEL;
   for (int b = t; b <= NB; b += NT) cnt[b] = 0;
-  br_part<6, false>(v1, dscr, 14, 0);
-  br_part<8, true>(mx, dscr, 14, 6);
-  br_fin<NT>(dscr, 14, 6);
+  fr_part_dpp<6, false>(v1, dscr, 14, 0);
+  fr_part_dpp<8, true>(mx, dscr, 14, 6);
+  fr_fin_dpp<NT>(dscr, 14, 6);
   const double* tot1 = dscr + NW * 14;        // sums [0,6), -min/max [6,14)
 #pragma unroll
   for (int q = 0; q < 6; ++q) v1[q] = tot1[q];
@@ -355,9 +355,9 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
         w[3] += dk * dy; w[4] += dk * dk;
         w[5] += fv * fv; w[6] += fv * r;
       }
-      br_part<7, false>(w, dscr, 14, 7 * m);
+      fr_part_dpp<7, false>(w, dscr, 14, 7 * m);
     }
-    br_fin<NT>(dscr, 14, 14);
+    fr_fin_dpp<NT>(dscr, 14, 14);
     if (t < 14) fin[t] = dscr[NW * 14 + t];
     __syncthreads();
   }
