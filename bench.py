@@ -44,7 +44,8 @@ def bytes_per_unit(stage, F):
 
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
-STAGE_KERNEL = {"ic_daily": "fmx::k_ic_daily_br<", "cs_rank": "fmx::k_cs_rank_br<",
+STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
+                "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",
                 "cs:market_neutralize": "fmx::k_cs_moment<2>", "ts:mean": "fmx::k_ts_reg<1,",
                 "ts:std": "fmx::k_ts_reg<2,", "ts:zscore": "fmx::k_ts_reg<4,", "ts:rank": "fmx::k_ts_reg<5,",
@@ -64,7 +65,7 @@ def pmc_traffic(stage, dims):
     key = ":".join(stage.split(":")[:2]).rstrip(":")
     pre = STAGE_KERNEL.get(key)
     for name, v in t.get("kernels", {}).items():
-        if pre and name.startswith(pre):
+        if pre and name.startswith(pre if isinstance(pre, tuple) else (pre,)):
             return v["traffic_bytes"]
     return None
 
