@@ -159,6 +159,18 @@ extern "C" fmx_status fmx_device_info(char* buf, int64_t buflen) {
   return FMX_OK;
 }
 
+namespace fmx {
+// Length (ints) of the schedule blob for n (cached; kernels stage short blobs in LDS).
+int pw_len(int n) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(n);
+  if (it == cache.end()) it = cache.emplace(n, (int)build_schedule(n).size()).first;
+  return it->second;
+}
+}  // namespace fmx
+
 // Test hook: copy the schedule blob for n into out (host), returns its length.
 extern "C" int32_t fmx_debug_pw_schedule(int32_t n, int32_t* out, int32_t cap) {
   std::vector<int32_t> s = build_schedule(n);

@@ -74,8 +74,9 @@ constexpr int CSM_NT = 512;
 template <int OP>
 __global__ void __launch_bounds__(CSM_NT)
 k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
-            const uint8_t* __restrict__ present, PwTable pw, double* __restrict__ stats) {
+            const uint8_t* __restrict__ present, PwTable pw, double* __restrict__ stats, int slen) {
   extern __shared__ double lds[];
+  __shared__ int32_t sch_l[PW_LDS_MAX];              // dense rows: the schedule for n = A
   const int64_t row = blockIdx.x;
   const int64_t d = row % D;
   const double* x = X + row * ld;
@@ -86,7 +87,14 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
   double* nodes = (double*)((char*)(v + A) + (present ? ((A * 2 + 15) & ~15) : 0));  // [2A/64+8]
   int* iscr = (int*)(nodes + (2 * (A / 64) + 8));
   int n;
+  const bool sch_lds = !prow && slen <= PW_LDS_MAX;
   if (!prow) {
+    // the schedule is staged with the row (same barrier): no global round trips inside
+    // the serial combine rounds
+    if (sch_lds) {
+      const int32_t* g = pw.get((int)A);
+      for (int i = threadIdx.x; i < slen; i += CSM_NT) sch_l[i] = g[i];
+    }
     for (int64_t i = threadIdx.x; i < A; i += CSM_NT) v[i] = x[i];
     __syncthreads();
     n = (int)A;
@@ -97,7 +105,7 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
     if (stats && threadIdx.x == 0) { stats[2 * row] = qnan(); stats[2 * row + 1] = qnan(); }
     return;
   }
-  const int32_t* sch = pw.get(n);
+  const int32_t* sch = sch_lds ? sch_l : pw.get(n);
   int cnt;
   const double s1 = block_pw_sum_w0<CSM_NT>([&](int i) { double t = v[i]; return t == t ? t : 0.0; },
                                             [&](int i) { return (int)(v[i] == v[i]); }, sch, nodes, iscr, &cnt);
@@ -509,7 +517,9 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
                                                  : (const void*)k_cs_moment<FMX_CS_STATS_ONLY>;
   if ((e = set_lds(k, lds))) return e;
   FMX_ARG(F * D <= 0x7fffffffll, "too many rows");
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats};
+  int slen = present ? PW_LDS_MAX + 1 : pw_len((int)A);
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats,
+                  (void*)&slen};
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(CSM_NT), args, lds, as_stream(stream)));
   return FMX_OK;
 }

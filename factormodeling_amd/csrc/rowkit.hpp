@@ -315,6 +315,10 @@ struct PwTable {
 };
 // Host: schedule table covering every n <= nmax on the current device (capi.hip).
 PwTable pw_table(int nmax, fmx_status* err);
+// Host: length in ints of the schedule blob for n.
+int pw_len(int n);
+// Schedules up to this many ints are staged in LDS by the dense-row moment kernels.
+constexpr int PW_LDS_MAX = 1024;
 
 // Host: bucket-rank launchers (rank_ops.hip).
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
