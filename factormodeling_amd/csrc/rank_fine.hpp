@@ -197,6 +197,8 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   uint8_t* bmask = (uint8_t*)(bkey + A);
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
+  // date-major rows: the F workgroups of a date share its return rows in L2 (measured
+  // faster than factor-major order at C2: 44.8 vs 46.5 ms)
   const int64_t s = blockIdx.x / F, f = blockIdx.x % F;
   const double* xf = X + (f * D + s) * ld;
   const int lagv[2] = {L0, L1};
@@ -205,7 +207,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     act[m] = m < NL && s + lagv[m] < D;
-    rr[m] = act[m] ? Rt + (s + lagv[m]) * ld : nullptr;
+    rr[m] = Rt + (act[m] ? s + lagv[m] : s) * ld;   // always a valid row
   }
   if (!act[0] && !act[1]) return;
   uint64_t key[EMAX];
@@ -215,13 +217,18 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   double mx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
+  // the row's exposures are all in flight before the first is consumed
+  const bool last_in = t + (EMAX - 1) * NT < A;
+  double xv[EMAX];
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) xv[k] = (k < EMAX - 1 || last_in) ? xf[t + k * NT] : qnan();
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const int64_t i = t + (int64_t)k * NT;
+    const int i = t + k * NT;
     key[k] = KEY_SENTINEL;
     pk[k] = 0;
-    if (i < A) {
-      const double v = xf[i];
+    {
+      const double v = xv[k];
       if (v == v) {
         int mm = 0;
 #pragma unroll
