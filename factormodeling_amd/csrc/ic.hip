@@ -124,7 +124,9 @@ __global__ void k_ic_window(const double* __restrict__ daily, int64_t F, int64_t
                             double* __restrict__ out) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= J * F) return;
-  const int64_t j = gid / F, f = gid % F;
+  // lanes walk consecutive jobs of one factor: rolling windows start on consecutive dates,
+  // so the daily-series reads of a wave are coalesced
+  const int64_t f = gid / J, j = gid % J;
   const int d0 = max(0, d0s[j]), d1 = min((int)D, d1s[j]);
   const double* dn = daily + (0 * F + f) * D;
   const double* dic = daily + (1 * F + f) * D;
@@ -151,7 +153,7 @@ __global__ void k_ic_window(const double* __restrict__ daily, int64_t F, int64_t
     if (b == b) v_ric += (b - m_ric) * (b - m_ric);
     if (c == c) v_b += (c - m_b) * (c - m_b);
   }
-  double* o = out + gid * 8;
+  double* o = out + (j * F + f) * 8;
   o[0] = m_ic;
   o[1] = n_ic > 1 ? m_ic / sqrt(v_ic / (n_ic - 1)) : qnan();
   o[2] = m_ric;

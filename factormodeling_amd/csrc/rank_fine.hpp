@@ -174,6 +174,189 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 }
 
 // ------------------------------------------------------------------------------------
+// cs_winsor (OP 0: clip to the quantiles when >= 5 non-NaN) / cs_filter_center (OP 1)
+// on fine buckets (operations.py:64-75).  The numpy 'linear' percentiles need four order
+// statistics; the fine-bucket histogram (one LDS atomic per element, one scan) locates
+// the bucket of each, and only the members of those (tiny) buckets are gathered and
+// ranked -- no per-element rank.  A bucket holding more than FR_QCAP members (heavily
+// clustered rows) falls back to a bisection of the key space with block counts.
+// LDS: the counters (32 KB) are dead once the four target buckets are known, and the
+// gathered lists reuse them: four rows per CU at 512 threads.
+constexpr int FR_QCAP = 1024;
+template <int OP, int NT, int EMAX, bool PRES>
+#ifndef FR_Q_WAVES
+#define FR_Q_WAVES 6
+#endif
+__global__ void __launch_bounds__(NT, FR_Q_WAVES)
+k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
+                 double qlo, double qhi, const uint8_t* __restrict__ present) {
+  constexpr int K = FR_K_CS, NW = NT / 64, NB = FRG<K>::NB;
+  constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;
+  static_assert(NB + 1 < DUMMY, "counter array");
+  static_assert(4 * FR_QCAP * 2 <= WORDS, "lists alias the counters");
+  __shared__ FrTab tab;
+  __shared__ uint4 wred[NW];
+  __shared__ int iscr[2 * (NW + 1)];
+  __shared__ int tfill[4];
+  __shared__ uint64_t tval[4];
+  extern __shared__ uint64_t lds[];           // WORDS packed counters, then 4 lists of keys
+  uint32_t* cnt = (uint32_t*)lds;
+  uint64_t* lists = lds;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t row = blockIdx.x;
+  const double* x = X + row * ld;
+  double* y = Y + row * ld;
+  const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
+  const int An = (int)A;
+  const bool last_in = t + (EMAX - 1) * NT < An;
+  uint64_t key[EMAX];
+  uint32_t pm = 0, hmin = 0xffffffffu, hmax = 0u;
+  int wv = 0;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const bool in = k < EMAX - 1 || last_in;
+    const double v = in ? x[t + k * NT] : 0.0;
+    const bool p = in && (PRES ? prow[t + k * NT] != 0 : true);
+    const bool ok = p && v == v;
+    pm |= (uint32_t)p << k;
+    key[k] = ok ? okey(v) : KEY_SENTINEL;
+    const uint32_t h = (uint32_t)(key[k] >> 32);
+    hmin = ok ? min(hmin, h) : hmin;
+    hmax = ok ? max(hmax, h) : hmax;
+    wv += __popcll(__ballot(ok));
+  }
+  fr_park_sample<NT, EMAX>(tab, key);
+#pragma unroll
+  for (int j = 0; j < WORDS / (4 * NT); ++j)
+    reinterpret_cast<uint4*>(cnt)[t * (WORDS / (4 * NT)) + j] = make_uint4(0u, 0u, 0u, 0u);
+  if (t < 4) tfill[t] = 0;
+  {
+    const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
+    if (lane == 0) wred[wid] = make_uint4(0u, (uint32_t)wv, a, c);
+  }
+  __syncthreads();
+  int nv = 0;
+  uint32_t h0 = 0xffffffffu, h1 = 0u;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const uint4 r = wred[w];
+    nv += (int)r.y;
+    h0 = min(h0, r.z);
+    h1 = max(h1, r.w);
+  }
+  double lo = qnan(), hi = qnan();
+  if (nv > 0 && (OP == 1 || nv >= 5)) {
+    if (wid == 0) {
+      double vmin, vmax;
+      fr_key_bounds(h0, h1, &vmin, &vmax);
+      fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
+    }
+    __syncthreads();
+    int bb[EMAX];
+    fr_bucket_all<K, EMAX>(tab, key, bb, DUMMY);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) fr_cnt_add(cnt, bb[k]);
+    __syncthreads();
+    fr_scan16<NT, WORDS>(cnt, iscr);
+    // order statistics (p, p+1) per quantile (numpy linear), identical when vi >= n-1
+    const double qs[2] = {qlo, qhi};
+    double gq[2];
+    int kk[4];
+#pragma unroll
+    for (int z = 0; z < 2; ++z) {
+      const double vi = (double)(nv - 1) * qs[z];
+      if (vi >= (double)(nv - 1)) {
+        kk[2 * z] = kk[2 * z + 1] = nv - 1;
+        gq[z] = vi + 1.0;
+      } else {
+        const double pf = floor(vi);
+        kk[2 * z] = (int)pf;
+        kk[2 * z + 1] = (int)pf + 1;
+        gq[z] = vi - pf;
+      }
+    }
+    // target bucket of each order statistic: last b with start[b] <= k (broadcast reads)
+    int tb[4], ts0[4], tn[4];
+    bool slow = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int l = 0, h = NB + 1;
+      while (l < h) {
+        const int m = (l + h) >> 1;
+        if ((int)fr_cnt_get(cnt, m) <= kk[j]) l = m + 1; else h = m;
+      }
+      tb[j] = l - 1;
+      ts0[j] = (int)fr_cnt_get(cnt, tb[j]);
+      tn[j] = (int)fr_cnt_get(cnt, tb[j] + 1) - ts0[j];
+      slow |= (tb[j] % (K + 1)) != K && tn[j] > FR_QCAP;
+    }
+    __syncthreads();                          // counters dead: the lists reuse their LDS
+    if (!slow) {
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (bb[k] == tb[j] && (tb[j] % (K + 1)) != K) lists[j * FR_QCAP + atomicAdd(&tfill[j], 1)] = key[k];
+      }
+      __syncthreads();
+      if (wid < 4) {
+        const int j = wid, b = tb[j];
+        if ((b % (K + 1)) == K) {
+          if (lane == 0) tval[j] = tab.spl[b / (K + 1)];
+        } else {
+          const uint64_t* L = lists + j * FR_QCAP;
+          const int n = tn[j], r = kk[j] - ts0[j];
+          for (int q = lane; q < n; q += 64) {
+            int lt, eq;
+            br_count(L, 0, n, L[q], &lt, &eq);
+            if (lt <= r && r < lt + eq) tval[j] = L[q];   // all writers store the same key
+          }
+        }
+      }
+      __syncthreads();
+    } else {
+      // bisection: smallest key v with #{keys <= v} > k
+      for (int j = 0; j < 4; ++j) {
+        uint64_t l = 0, h = KEY_SENTINEL - 1;
+        while (l < h) {
+          const uint64_t m = l + ((h - l) >> 1);
+          int c = 0;
+#pragma unroll
+          for (int k = 0; k < EMAX; ++k) c += key[k] <= m;   // sentinel > m always
+          br_sum<NT, 1, int>(&c, iscr);
+          if (c > kk[j]) h = m; else l = m + 1;
+        }
+        if (t == 0) tval[j] = l;
+      }
+      __syncthreads();
+    }
+    double qv[2];
+#pragma unroll
+    for (int z = 0; z < 2; ++z) {
+      const double a = okey_inv(tval[2 * z]), b = okey_inv(tval[2 * z + 1]);
+      const double g = gq[z];
+      const double diff = b - a;
+      qv[z] = (g >= 0.5) ? b - diff * (1.0 - g) : a + diff * g;
+    }
+    lo = qv[0];
+    hi = qv[1];
+  }
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    if (!(k < EMAX - 1 || last_in)) continue;
+    const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+    double o;
+    if (OP == 0) {
+      o = v;
+      if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
+    } else {
+      o = (v < lo || v > hi) ? v : 0.0;
+    }
+    y[t + k * NT] = (PRES && !((pm >> k) & 1)) ? qnan() : o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Fused daily IC: workgroup (source row s, factor f) ranks X[f][s] once and produces the
 // stats of the pairs (X[f][s], R[s + L_m]) for up to two lags.  Bucket members are the
 // exposures pair-valid for at least one lag; one 64-bit counter per bucket packs
