@@ -149,6 +149,60 @@ __device__ __forceinline__ void fr_part_dpp(const double* v, double* scr, int S,
     if (lane == 0) scr[wid * S + off + i] = x;
   }
 }
+// Multi-value butterfly (same contract as fr_part_dpp, N in {2, 4, 8, 16}): each DPP
+// exchange step halves the values a lane carries (it keeps one half, sends the other to
+// its partner), so N values cost N-1 exchanges inside the 16-lane rows instead of 4N,
+// then two cross-row swaps.  Lane bits 3..0 pick the half (row mirror, half-row mirror,
+// quad xor 2, xor 1 are all involutions that flip those bits).
+template <bool MAX>
+__device__ __forceinline__ double fr_op2(double a, double b) { return MAX ? fmax(a, b) : a + b; }
+template <int CTRL, int H, bool MAX>
+__device__ __forceinline__ void fr_bfly_step(double* v, bool upper) {
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const double send = upper ? v[i] : v[i + H];
+    const double keep = upper ? v[i + H] : v[i];
+    v[i] = fr_op2<MAX>(keep, fr_dpp_d<CTRL>(send));
+  }
+}
+template <int N, bool MAX>
+__device__ __forceinline__ void fr_part_bfly(const double* vin, double* scr, int S, int off) {
+  static_assert(N == 2 || N == 4 || N == 8 || N == 16, "N");
+  constexpr int LG = N == 2 ? 1 : N == 4 ? 2 : N == 8 ? 3 : 4;
+  const int lane = fr_lane(), wid = threadIdx.x >> 6;
+  double v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = vin[i];
+  if constexpr (LG >= 4) fr_bfly_step<0x140, N / 2, MAX>(v, lane & 8);
+  else v[0] = v[0];
+  if constexpr (LG == 4) fr_bfly_step<0x141, N / 4, MAX>(v, lane & 4);
+  if constexpr (LG == 4) fr_bfly_step<0x4E, N / 8, MAX>(v, lane & 2);
+  if constexpr (LG == 4) fr_bfly_step<0xB1, N / 16, MAX>(v, lane & 1);
+  if constexpr (LG == 3) {
+    fr_bfly_step<0x140, 4, MAX>(v, lane & 8);
+    fr_bfly_step<0x141, 2, MAX>(v, lane & 4);
+    fr_bfly_step<0x4E, 1, MAX>(v, lane & 2);
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0xB1>(v[0]));
+  }
+  if constexpr (LG == 2) {
+    fr_bfly_step<0x140, 2, MAX>(v, lane & 8);
+    fr_bfly_step<0x141, 1, MAX>(v, lane & 4);
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0x4E>(v[0]));
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0xB1>(v[0]));
+  }
+  if constexpr (LG == 1) {
+    fr_bfly_step<0x140, 1, MAX>(v, lane & 8);
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0x141>(v[0]));
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0x4E>(v[0]));
+    v[0] = fr_op2<MAX>(v[0], fr_dpp_d<0xB1>(v[0]));
+  }
+  // row r of the wave now holds, in lane 16r + j, its partial of value (j >> (4 - LG))
+  double x = v[0];
+  x = fr_op2<MAX>(x, fr_xor_d(x, 16, lane));
+  x = fr_op2<MAX>(x, fr_xor_d(x, 32, lane));
+  if (lane < 16 && (lane & ((16 >> LG) - 1)) == 0) scr[wid * S + off + (lane >> (4 - LG))] = x;
+}
+
 template <int NT>
 __device__ __forceinline__ void fr_fin_dpp(double* scr, int S, int nsum) {
   constexpr int NR = NT / 64;

@@ -375,7 +375,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   __shared__ FrTab tab;
   __shared__ u64 cnt[NB + 1];
   __shared__ u64 uscr[NW];
-  __shared__ double dscr[(NW + 1) * 14];
+  __shared__ double dscr[(NW + 1) * 16];
   extern __shared__ uint64_t bkey[];          // A keys, then A mask bytes
   uint8_t* bmask = (uint8_t*)(bkey + A);
   const int t = threadIdx.x, wid = t >> 6;
@@ -396,7 +396,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   uint64_t key[EMAX];
   int pk[EMAX];                               // mask << FR_MSH, later slot | bucket
   // v1: n per lag, sum f per lag, sum r per lag;  mx: -min f, max f, -min r, max r per lag
-  double v1[6] = {0, 0, 0, 0, 0, 0};
+  double v1[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // [6, 8): butterfly padding
   double mx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
@@ -434,25 +434,25 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   }
   const uint64_t smp = wid == 0 ? fr_sample(xf, nullptr, A) : KEY_SENTINEL;
   for (int b = t; b <= NB; b += NT) cnt[b] = 0;
-  fr_part_dpp<6, false>(v1, dscr, 14, 0);
-  fr_part_dpp<8, true>(mx, dscr, 14, 6);
-  fr_fin_dpp<NT>(dscr, 14, 6);
-  const double* tot1 = dscr + NW * 14;        // sums [0,6), -min/max [6,14)
+  fr_part_bfly<8, false>(v1, dscr, 16, 0);
+  fr_part_bfly<8, true>(mx, dscr, 16, 8);
+  fr_fin_dpp<NT>(dscr, 16, 8);
+  const double* tot1 = dscr + NW * 16;        // sums [0,6), -min/max [8,16)
 #pragma unroll
   for (int q = 0; q < 6; ++q) v1[q] = tot1[q];
   BR_PH();
   __shared__ double cst[8];                   // only thread 0 reads them back
   if (t == 0) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) cst[q] = tot1[6 + q];
+    for (int q = 0; q < 8; ++q) cst[q] = tot1[8 + q];
   }
   const int n[2] = {(int)v1[0], (int)v1[1]};
   const bool need = (act[0] && n[0] >= 3) || (act[1] && n[1] >= 3);
-  __shared__ double fin[14];                  // per-lag moment totals (thread 0)
+  __shared__ double fin[16];                  // per-lag moment totals (thread 0)
   if (need) {
     if (wid == 0) {
       // bounds of the union of both lags' members (empty lag: -min = max = -inf)
-      const double vmin = -fmax(tot1[6], tot1[10]), vmax = fmax(tot1[7], tot1[11]);
+      const double vmin = -fmax(tot1[8], tot1[12]), vmax = fmax(tot1[9], tot1[13]);
       fr_build_w0<K>(tab, smp, vmin, vmax);
     }
     __syncthreads();
@@ -531,7 +531,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
     // one lag at a time keeps 7 accumulators live
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      double w[7] = {0, 0, 0, 0, 0, 0, 0};
+      double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int k = 0; k < EMAX; ++k) {
         if (!((msk[k] >> m) & 1)) continue;
@@ -545,10 +545,10 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
         w[3] += dk * dy; w[4] += dk * dk;
         w[5] += fv * fv; w[6] += fv * r;
       }
-      fr_part_dpp<7, false>(w, dscr, 14, 7 * m);
+      fr_part_bfly<8, false>(w, dscr, 16, 8 * m);
     }
-    fr_fin_dpp<NT>(dscr, 14, 14);
-    if (t < 14) fin[t] = dscr[NW * 14 + t];
+    fr_fin_dpp<NT>(dscr, 16, 16);
+    if (t < 16) fin[t] = dscr[NW * 16 + t];
     __syncthreads();
   }
   if (t == 0) {
@@ -561,7 +561,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
       const int nn = n[m];
       double ic = qnan(), ric = qnan(), beta = qnan();
       if (nn >= 3) {
-        const double* w = fin + 7 * m;
+        const double* w = fin + 8 * m;
         const bool fconst = (-cst[4 * m + 0]) == cst[4 * m + 1];
         const bool rconst = (-cst[4 * m + 2]) == cst[4 * m + 3];
         if (!fconst && !rconst) {
