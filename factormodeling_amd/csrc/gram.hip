@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <cstdlib>
+
 #include "rowkit.hpp"
 
 namespace fmx {
@@ -271,7 +273,8 @@ typedef float flt4 __attribute__((ext_vector_type(4)));
 template <int NB, int MODE>   // MODE 0: G = Z Z^T on fp64 MFMA; 1: N = M M^T on bf16 MFMA
 __global__ void __launch_bounds__(SG_NT)
 k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
-             int64_t ld, int64_t d0, int64_t d1, int64_t dps, double* __restrict__ part) {
+             int64_t ld, int64_t d0, int64_t d1, int64_t dps, double* __restrict__ part,
+             uint32_t* __restrict__ mbits) {
   constexpr int FP = 16 * NB;
   constexpr int NTRI = NB * (NB + 1) / 2;
   constexpr int NWV = SG_NT / 64;
@@ -304,8 +307,11 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
   const int64_t nch = (A + SG_K - 1) / SG_K;
   const int64_t total = (de - ds) * nch;
   double xr[EPT];
-  auto issue = [&](int64_t c) {
-    const int64_t d = ds + c / nch, a0 = (c % nch) * SG_K;
+  // chunk (date, asset block) walked by counters (no 64-bit divides in the loop)
+  int64_t nd_iss = ds, na_iss = 0;               // next chunk to issue
+  auto issue = [&]() {
+    const int64_t d = nd_iss, a0 = na_iss * SG_K;
+    if (++na_iss == nch) { na_iss = 0; ++nd_iss; }
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
       const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
@@ -320,22 +326,32 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
     }
   };
   if (total > 0) {
-    issue(0);
+    issue();
     load_stats(ds);
   }
+  // mask word of chunk c for row r: r * mstride + mword (32-bit: F * dates * A/32 < 2^32)
+  const uint32_t mstride = (uint32_t)((d1 - d0) * nch);
+  uint32_t mword = (uint32_t)((ds - d0) * nch);
+  int64_t cin = 0, dcur = ds;                    // chunk c's asset block and date
   __syncthreads();
   for (int64_t c = 0; c < total; ++c) {
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
       const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
-      if (e >= NEL) continue;
+      if (e >= NEL) continue;                   // wave-uniform (NEL is a multiple of 64)
       const double v = xr[u], sd = sd_s[r];
       const bool ok = (v == v) && (sd > 0.0);
       if (MODE == 0) Zs[r * SG_KP + cl] = ok ? (v - mu_s[r]) / sd : 0.0;
       else Ms[r * SG_MP + cl] = ok ? (uint16_t)0x3f80 : (uint16_t)0;   // bf16 1.0 / 0.0
+      if (MODE == 0 && mbits) {
+        // the chunk's validity bits, one 32-asset word per row (lanes 0-31: row r, 32-63:
+        // row r+1): the pair counts N = M M^T come from these by AND + popcount
+        const uint64_t bal = __ballot(ok);
+        if ((lane & 31) == 0 && r < F) mbits[(uint32_t)r * mstride + mword] = (uint32_t)(bal >> lane);
+      }
     }
     __syncthreads();
-    if (c + 1 < total) issue(c + 1);
+    if (c + 1 < total) issue();
     if (MODE == 0) {
 #pragma unroll 1
       for (int ks = 0; ks < SG_K; ks += 4) {     // not unrolled: bounds the fragment registers
@@ -360,7 +376,8 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
       }
     }
     // the stats of chunk c were consumed before the barrier above
-    if (c + 1 < total && (c + 1) % nch == 0) load_stats(ds + (c + 1) / nch);
+    if (c + 1 < total && ++cin == nch) { cin = 0; load_stats(++dcur); }
+    ++mword;
     __syncthreads();
   }
   double* p = part + slice * (int64_t)FP * FP;
@@ -380,7 +397,8 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
 // Sum the slices in order (deterministic) for the upper-triangle blocks and mirror.
 __global__ void k_gram_small_reduce(const double* __restrict__ partG, const double* __restrict__ partN,
                                     int64_t nslice, int FP, int64_t F, double* __restrict__ G,
-                                    double* __restrict__ N, int accumulate) {
+                                    double* __restrict__ N, int accumulate,
+                                    const unsigned long long* __restrict__ ncnt) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)FP * FP) return;
   const int i = (int)(e / FP), j = (int)(e % FP);
@@ -390,8 +408,9 @@ __global__ void k_gram_small_reduce(const double* __restrict__ partG, const doub
 #pragma unroll 8
   for (int64_t sl = 0; sl < nslice; ++sl) {
     g += partG[sl * st + e];
-    n += partN[sl * st + e];
+    if (!ncnt) n += partN[sl * st + e];
   }
+  if (ncnt) n = (double)ncnt[e];
   if (accumulate) {
     g += G[(int64_t)i * F + j];
     n += N[(int64_t)i * F + j];
@@ -400,6 +419,46 @@ __global__ void k_gram_small_reduce(const double* __restrict__ partG, const doub
   G[(int64_t)j * F + i] = g;
   N[(int64_t)i * F + j] = n;
   N[(int64_t)j * F + i] = n;
+}
+
+// N = M M^T from the validity bits k_gram_small<.,0> packed (32 assets per word): one
+// workgroup per (32 x 32 tile of the upper triangle, word range); 64-word chunks of the
+// 64 rows staged in LDS, each thread owns one row i and four rows j.  Integer counts:
+// exact, and order-free (64-bit atomics into ncnt[FP][FP]).
+constexpr int PC_W = 64;
+__global__ void __launch_bounds__(256)
+k_gram_popc(const uint32_t* __restrict__ mbits, int64_t F, int64_t nw, int64_t wps, int FP,
+            unsigned long long* __restrict__ ncnt) {
+  __shared__ uint32_t Ai[32][PC_W + 1], Bj[32][PC_W + 1];
+  const int tid = threadIdx.x;
+  int tt = blockIdx.x, ti = 0;
+  const int T = (int)((F + 31) / 32);
+  while (tt >= T - ti) { tt -= T - ti; ++ti; }
+  const int I0 = ti * 32, J0 = (ti + tt) * 32;
+  const int64_t w0 = (int64_t)blockIdx.y * wps, w1 = min<int64_t>(nw, w0 + wps);
+  const int i = tid >> 3, jg = tid & 7;
+  unsigned acc[4] = {0u, 0u, 0u, 0u};
+  for (int64_t wc = w0; wc < w1; wc += PC_W) {
+    for (int q = tid; q < 32 * PC_W; q += 256) {
+      const int r = q / PC_W, w = q % PC_W;
+      const bool in = wc + w < w1;
+      Ai[r][w] = (in && I0 + r < F) ? mbits[(int64_t)(I0 + r) * nw + wc + w] : 0u;
+      Bj[r][w] = (in && J0 + r < F) ? mbits[(int64_t)(J0 + r) * nw + wc + w] : 0u;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int w = 0; w < PC_W; ++w) {
+      const uint32_t a = Ai[i][w];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += __popc(a & Bj[jg + 8 * k][w]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int gi = I0 + i, gj = J0 + jg + 8 * k;
+    if (gi < F && gj < F && acc[k]) atomicAdd(&ncnt[(int64_t)gi * FP + gj], (unsigned long long)acc[k]);
+  }
 }
 
 template <int NB>
@@ -413,15 +472,41 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   nslice = ceil_div(ndates, dps);
   double* part = nullptr;
   const int64_t st_elems = (int64_t)FP * FP * nslice;
-  FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * st_elems, st));
-  k_gram_small<NB, 0><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part);
+  // pair counts: validity bits packed by the fp64 pass + AND/popcount (default), or the
+  // bf16 MFMA pass over the panel (FMX_GRAM_MASK_MFMA=1, kept for A/B)
+  static const bool mask_mfma = getenv("FMX_GRAM_MASK_MFMA") != nullptr;
+  const int64_t nchw = ceil_div(A, (int64_t)SG_K), nw = ndates * nchw;
+  uint32_t* mbits = nullptr;
+  unsigned long long* ncnt = nullptr;
+  if (mask_mfma) {
+    FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * st_elems, st));
+  } else {
+    FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * st_elems, st));
+    FMX_HIP(hipMallocAsync((void**)&mbits, sizeof(uint32_t) * F * nw, st));
+    FMX_HIP(hipMallocAsync((void**)&ncnt, sizeof(unsigned long long) * FP * FP, st));
+    FMX_HIP(hipMemsetAsync(ncnt, 0, sizeof(unsigned long long) * FP * FP, st));
+  }
+  k_gram_small<NB, 0><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part, mbits);
   FMX_LAUNCH_CHECK("k_gram_small<G>");
-  k_gram_small<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part + st_elems);
-  FMX_LAUNCH_CHECK("k_gram_small<N>");
-  k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(part, part + st_elems, nslice, FP,
-                                                                                  F, G, N, accumulate);
+  if (mask_mfma) {
+    k_gram_small<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part + st_elems,
+                                                           nullptr);
+    FMX_LAUNCH_CHECK("k_gram_small<N>");
+  } else if (nw > 0) {
+    const int T = (int)ceil_div(F, (int64_t)32);
+    const int ntile = T * (T + 1) / 2;
+    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PC_W), 2048 / ntile + 1));
+    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PC_W) * PC_W;
+    const unsigned nky = (unsigned)ceil_div(nw, wps);
+    k_gram_popc<<<dim3((unsigned)ntile, nky), 256, 0, st>>>(mbits, F, nw, wps, FP, ncnt);
+    FMX_LAUNCH_CHECK("k_gram_popc");
+  }
+  k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(
+      part, mask_mfma ? part + st_elems : nullptr, nslice, FP, F, G, N, accumulate, mask_mfma ? nullptr : ncnt);
   FMX_LAUNCH_CHECK("k_gram_small_reduce");
   FMX_HIP(hipFreeAsync(part, st));
+  if (mbits) FMX_HIP(hipFreeAsync(mbits, st));
+  if (ncnt) FMX_HIP(hipFreeAsync(ncnt, st));
   return FMX_OK;
 }
 
