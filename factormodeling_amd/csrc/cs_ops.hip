@@ -5,7 +5,13 @@
 // Reference: operations.py:54-86 (cs_rank, cs_winsor, cs_filter_center, cs_zscore,
 // cs_bool, cs_mean), :88-101 (elementwise), :104-168 (bucket, group ops), :171-182
 // (market_neutralize), :248-304 (cs_regression).
+#include <vector>
+#include <map>
+#include <mutex>
+#include <cstdlib>
 #include "rowkit.hpp"
+
+extern "C" int32_t fmx_debug_pw_schedule(int32_t n, int32_t* out, int32_t cap);
 
 namespace fmx {
 
@@ -137,6 +143,132 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
   if (prow) {
     for (int64_t a = threadIdx.x; a < A; a += CSM_NT)
       if (!prow[a]) y[a] = qnan();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Dense rows, register-resident variant of k_cs_moment (same numpy pairwise order, bit-
+// identical).  Lane (leaf = tid / 8, j = tid % 8) loads exactly the elements its numpy
+// accumulator adds -- leaf start + j + 8i -- straight from HBM into registers (8 lanes
+// read 64 contiguous bytes), so the row is never staged in LDS: a workgroup holds only the
+// schedule (staged once, the workgroup is persistent over rows) and the 2L leaf nodes,
+// and occupancy is set by registers.  Requires L <= CSR_NT / 8 leaves of <= 128 elements.
+constexpr int CSR_NT = 512;
+constexpr int CSR_EL = 16;            // elements per lane: leaves hold <= 128 = 8 x 16
+template <int OP>
+__global__ void __launch_bounds__(CSR_NT, 8)
+k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
+               PwTable pw, int slen, double* __restrict__ stats) {
+  __shared__ int32_t sch[PW_LDS_MAX];
+  __shared__ double nodes[2 * (CSR_NT / 8) + 8];
+  __shared__ int iscr[CSR_NT / 64 + 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  {
+    const int32_t* g = pw.get((int)A);
+    for (int i = tid; i < slen; i += CSR_NT) sch[i] = g[i];
+  }
+  __syncthreads();
+  PwView sv{sch};
+  const int L = sv.L(), R = sv.R();
+  const int leaf = tid >> 3, j = tid & 7;
+  const bool act = leaf < L;
+  const int st = act ? sv.lstart(leaf) : 0, len = act ? sv.llen(leaf) : 0;
+  const int stop = len - (len & 7), nfull = stop >> 3;
+  const int32_t* tr = sv.trip();
+  // combine rounds of wave 0 (the schedule's tree), result in nodes[0]
+  auto combine = [&]() {
+    if (wid == 0) {
+      for (int rr = 0; rr < R; ++rr) {
+        for (int q = sv.roff(rr) + lane; q < sv.roff(rr + 1); q += 64)
+          nodes[tr[3 * q]] = nodes[tr[3 * q + 1]] + nodes[tr[3 * q + 2]];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      if (lane == 0) nodes[0] = nodes[sv.root()];
+    }
+  };
+  for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+    const double* x = X + row * ld;
+    double xv[CSR_EL];
+#pragma unroll
+    for (int i = 0; i < CSR_EL; ++i) xv[i] = (i < nfull) ? x[st + j + 8 * i] : 0.0;
+    // sum 1: numpy nansum (NaN -> 0) and the valid count
+    double r = 0.0;
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < CSR_EL; ++i) {
+      if (i < nfull) {
+        const double t = xv[i];
+        const double z = t == t ? t : 0.0;
+        r = i == 0 ? z : r + z;
+        c += t == t;
+      }
+    }
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (act && j == 0) {
+      for (int q = stop; q < len; ++q) { const double t = x[st + q]; r += t == t ? t : 0.0; c += t == t; }
+      nodes[leaf] = r;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) iscr[wid] = c;
+    __syncthreads();
+    combine();
+    if (tid == 0) {
+      int tot = 0;
+      for (int w = 0; w < CSR_NT / 64; ++w) tot += iscr[w];
+      iscr[CSR_NT / 64] = tot;
+    }
+    __syncthreads();
+    const int cnt = iscr[CSR_NT / 64];
+    const double mean = cnt > 0 ? nodes[0] / (double)cnt : qnan();
+    double sd = 0.0;
+    if (OP != FMX_CS_MEAN) {
+      __syncthreads();                                 // nodes[0] read by everyone
+      double q2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < CSR_EL; ++i) {
+        if (i < nfull) {
+          const double t = xv[i];
+          const double z = t == t ? t : 0.0;
+          const double q = t == t ? (mean - z) * (mean - z) : 0.0;
+          q2 = i == 0 ? q : q2 + q;
+        }
+      }
+      q2 = q2 + __shfl_xor(q2, 1);
+      q2 = q2 + __shfl_xor(q2, 2);
+      q2 = q2 + __shfl_xor(q2, 4);
+      if (act && j == 0) {
+        for (int q = stop; q < len; ++q) {
+          const double t = x[st + q];
+          const double z = t == t ? t : 0.0;
+          q2 += t == t ? (mean - z) * (mean - z) : 0.0;
+        }
+        nodes[leaf] = q2;
+      }
+      __syncthreads();
+      combine();
+      __syncthreads();
+      const double var = cnt > 0 ? nodes[0] / (double)cnt : qnan();
+      sd = sqrt(var);
+    }
+    if (stats && tid == 0) { stats[2 * row] = cnt > 0 ? mean : qnan(); stats[2 * row + 1] = cnt > 0 ? sd : qnan(); }
+    if (OP != FMX_CS_STATS_ONLY) {
+      const bool guard = (OP == FMX_CS_MARKET_NEUTRALIZE) && (sd == 0.0 || sd != sd);
+      auto outv = [&](double t) {
+        if (OP == FMX_CS_MEAN) return mean;
+        if (guard) return 0.0;
+        return (t - mean) / sd;
+      };
+      double* y = Y + row * ld;
+#pragma unroll
+      for (int i = 0; i < CSR_EL; ++i)
+        if (i < nfull) y[st + j + 8 * i] = outv(xv[i]);
+      if (act && j == 0)
+        for (int q = stop; q < len; ++q) y[st + q] = outv(x[st + q]);
+    }
+    __syncthreads();                                   // nodes / iscr reused by the next row
   }
 }
 
@@ -518,6 +650,41 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
   if ((e = set_lds(k, lds))) return e;
   FMX_ARG(F * D <= 0x7fffffffll, "too many rows");
   int slen = present ? PW_LDS_MAX + 1 : pw_len((int)A);
+  // dense rows whose numpy leaves fit one 512-thread workgroup: register-resident kernel
+  static const bool no_rg = getenv("FMX_CS_MOMENT_LDS") != nullptr;
+  if (!present && slen <= PW_LDS_MAX && !no_rg && A >= 8) {
+    std::vector<int32_t> sh(slen);
+    fmx_debug_pw_schedule((int32_t)A, sh.data(), slen);
+    bool fits = sh[1] > 0 && sh[1] <= CSR_NT / 8;
+    for (int k = 0; fits && k < sh[1]; ++k) fits = sh[5 + sh[1] + k] <= 8 * CSR_EL;
+    if (fits) {
+      const void* kr = op == FMX_CS_ZSCORE ? (const void*)k_cs_moment_rg<FMX_CS_ZSCORE>
+                     : op == FMX_CS_MEAN ? (const void*)k_cs_moment_rg<FMX_CS_MEAN>
+                     : op == FMX_CS_MARKET_NEUTRALIZE ? (const void*)k_cs_moment_rg<FMX_CS_MARKET_NEUTRALIZE>
+                                                      : (const void*)k_cs_moment_rg<FMX_CS_STATS_ONLY>;
+      static std::map<const void*, int64_t> slots_cache;
+      static std::mutex mu;
+      int64_t slots;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = slots_cache.find(kr);
+        if (it == slots_cache.end()) {
+          int dev = 0, cus = 0, per = 0;
+          FMX_HIP(hipGetDevice(&dev));
+          FMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+          FMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kr, CSR_NT, 0));
+          it = slots_cache.emplace(kr, (int64_t)std::max(1, per) * std::max(1, cus)).first;
+        }
+        slots = it->second;
+      }
+      const int64_t nrows = F * D;
+      const int64_t grid = std::min<int64_t>(nrows, slots);
+      void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
+                       (void*)&stats};
+      FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
+      return FMX_OK;
+    }
+  }
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats,
                   (void*)&slen};
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(CSM_NT), args, lds, as_stream(stream)));

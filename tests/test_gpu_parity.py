@@ -276,3 +276,25 @@ def test_corr_gram_fused_date_range(fm):
     X[rng.random(X.shape) < 0.1] = np.nan
     C = E.corr_matrix(torch.as_tensor(X, device="cuda"), 2, 7).cpu().numpy()
     np.testing.assert_allclose(C, OG.corr_matrix(X, 2, 7), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("A", [9, 129, 2500, 4097, 5000, 8200, 10000])
+def test_cs_moment_row_lengths_vs_oracle(fm, A):
+    """cs_zscore / market_neutralize bit-exact at the row lengths that pick the register-
+    resident kernel (numpy leaves fit 64 x 8 lanes) and the LDS kernel (longer rows)."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.ops as O
+    rng = np.random.default_rng(A)
+    X = rng.standard_normal((2, 6, A))
+    X = np.where(rng.random(X.shape) < 0.2, np.round(X, 1), X)
+    X[rng.random(X.shape) < 0.02] = np.nan
+    X[0, 3] = np.nan                          # empty row
+    X[1, 2] = -1.25                           # constant row
+    Xd = torch.as_tensor(X, device="cuda")
+    for op, ref_fn in (("zscore", O.cs_zscore), ("market_neutralize", O.market_neutralize)):
+        got = E.cs_moment(op, Xd).cpu().numpy()
+        for f in range(2):
+            with np.errstate(all="ignore"):
+                ref = ref_fn(X[f])
+            assert_close(got[f].ravel(), ref.ravel(), exact=True, what=f"{op} A={A}")
