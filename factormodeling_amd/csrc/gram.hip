@@ -329,8 +329,8 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
     issue();
     load_stats(ds);
   }
-  // mask word of chunk c for row r: r * mstride + mword (32-bit: F * dates * A/32 < 2^32)
-  const uint32_t mstride = (uint32_t)((d1 - d0) * nch);
+  // mask word of chunk c for row r: mword * F + r, word-major so that a chunk's rows are
+  // one contiguous run (32-bit: F * dates * A/32 < 2^32)
   uint32_t mword = (uint32_t)((ds - d0) * nch);
   int64_t cin = 0, dcur = ds;                    // chunk c's asset block and date
   __syncthreads();
@@ -347,7 +347,7 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
         // the chunk's validity bits, one 32-asset word per row (lanes 0-31: row r, 32-63:
         // row r+1): the pair counts N = M M^T come from these by AND + popcount
         const uint64_t bal = __ballot(ok);
-        if ((lane & 31) == 0 && r < F) mbits[(uint32_t)r * mstride + mword] = (uint32_t)(bal >> lane);
+        if ((lane & 31) == 0 && r < F) mbits[mword * (uint32_t)F + (uint32_t)r] = (uint32_t)(bal >> lane);
       }
     }
     __syncthreads();
@@ -421,7 +421,8 @@ __global__ void k_gram_small_reduce(const double* __restrict__ partG, const doub
   N[(int64_t)j * F + i] = n;
 }
 
-// N = M M^T from the validity bits k_gram_small<.,0> packed (32 assets per word): one
+// N = M M^T from the validity bits k_gram_small<.,0> packed (32 assets per word, stored
+// word-major [word][F]): one
 // workgroup per (32 x 32 tile of the upper triangle, word range); 64-word chunks of the
 // 64 rows staged in LDS, each thread owns one row i and four rows j.  Integer counts:
 // exact, and order-free (64-bit atomics into ncnt[FP][FP]).
@@ -440,10 +441,10 @@ k_gram_popc(const uint32_t* __restrict__ mbits, int64_t F, int64_t nw, int64_t w
   unsigned acc[4] = {0u, 0u, 0u, 0u};
   for (int64_t wc = w0; wc < w1; wc += PC_W) {
     for (int q = tid; q < 32 * PC_W; q += 256) {
-      const int r = q / PC_W, w = q % PC_W;
+      const int r = q & 31, w = q >> 5;          // word-major bits: 32 rows of a word are contiguous
       const bool in = wc + w < w1;
-      Ai[r][w] = (in && I0 + r < F) ? mbits[(int64_t)(I0 + r) * nw + wc + w] : 0u;
-      Bj[r][w] = (in && J0 + r < F) ? mbits[(int64_t)(J0 + r) * nw + wc + w] : 0u;
+      Ai[r][w] = (in && I0 + r < F) ? mbits[(wc + w) * F + I0 + r] : 0u;
+      Bj[r][w] = (in && J0 + r < F) ? mbits[(wc + w) * F + J0 + r] : 0u;
     }
     __syncthreads();
 #pragma unroll 8
