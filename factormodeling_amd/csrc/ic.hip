@@ -169,6 +169,61 @@ __global__ void k_ic_window(const double* __restrict__ daily, int64_t F, int64_t
   o[7] = (double)n_days;
 }
 
+// Long windows with few (job, factor) pairs (the full-sample summary: J = 1, so only F
+// lanes would walk ~D days each): one 256-thread block per pair, block-reduced sums; same
+// outputs as k_ic_window (summation order differs: tolerance-level, not bit-level).
+__global__ void __launch_bounds__(256)
+k_ic_window_blk(const double* __restrict__ daily, int64_t F, int64_t D, const int32_t* __restrict__ d0s,
+                const int32_t* __restrict__ d1s, int64_t J, double* __restrict__ out) {
+  __shared__ double scr[16];
+  const int64_t j = blockIdx.x / F, f = blockIdx.x % F;
+  const int d0 = max(0, d0s[j]), d1 = min((int)D, d1s[j]);
+  const double* dn = daily + (0 * F + f) * D;
+  const double* dic = daily + (1 * F + f) * D;
+  const double* dric = daily + (2 * F + f) * D;
+  const double* db = daily + (3 * F + f) * D;
+  double s_ic = 0, s_ric = 0, s_b = 0, n_ic = 0, n_ric = 0, n_b = 0, n_days = 0, n_pos = 0;
+  for (int d = d0 + (int)threadIdx.x; d < d1; d += 256) {
+    if (dn[d] < 3.0) continue;
+    n_days += 1;
+    const double a = dic[d], b = dric[d], c = db[d];
+    if (a == a) { s_ic += a; n_ic += 1; }
+    if (b == b) { s_ric += b; n_ric += 1; }
+    if (c == c) { s_b += c; n_b += 1; n_pos += (c > 0); }
+  }
+  s_ic = block_sum<256>(s_ic, scr); s_ric = block_sum<256>(s_ric, scr); s_b = block_sum<256>(s_b, scr);
+  n_ic = block_sum<256>(n_ic, scr); n_ric = block_sum<256>(n_ric, scr); n_b = block_sum<256>(n_b, scr);
+  n_days = block_sum<256>(n_days, scr); n_pos = block_sum<256>(n_pos, scr);
+  const double m_ic = n_ic > 0 ? s_ic / n_ic : qnan();
+  const double m_ric = n_ric > 0 ? s_ric / n_ric : qnan();
+  const double m_b = n_b > 0 ? s_b / n_b : qnan();
+  double v_ic = 0, v_ric = 0, v_b = 0;
+  for (int d = d0 + (int)threadIdx.x; d < d1; d += 256) {
+    if (dn[d] < 3.0) continue;
+    const double a = dic[d], b = dric[d], c = db[d];
+    if (a == a) v_ic += (a - m_ic) * (a - m_ic);
+    if (b == b) v_ric += (b - m_ric) * (b - m_ric);
+    if (c == c) v_b += (c - m_b) * (c - m_b);
+  }
+  v_ic = block_sum<256>(v_ic, scr); v_ric = block_sum<256>(v_ric, scr); v_b = block_sum<256>(v_b, scr);
+  if (threadIdx.x == 0) {
+    double* o = out + (j * F + f) * 8;
+    o[0] = m_ic;
+    o[1] = n_ic > 1 ? m_ic / sqrt(v_ic / (n_ic - 1)) : qnan();
+    o[2] = m_ric;
+    o[3] = n_ric > 1 ? m_ric / sqrt(v_ric / (n_ric - 1)) : qnan();
+    if (n_b > 1) {
+      const double var = (v_b / n_b) * (n_b / (n_b - 1));
+      o[4] = m_b / sqrt(var / n_b);
+    } else {
+      o[4] = qnan();
+    }
+    o[5] = n_b;
+    o[6] = n_b > 0 ? n_pos / n_b : qnan();
+    o[7] = n_days;
+  }
+}
+
 // icir_top over J days.  metrics [J][F][8]; col 1 (IC_IR) or 3 (rank_IC_IR).
 // order_out [J][F]: factor index at each sorted position.  w_out [J][F] (factor order).
 __global__ void k_select_icir_top(const double* __restrict__ metrics, int64_t J, int64_t F, int col,
@@ -269,6 +324,11 @@ extern "C" fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, c
   FMX_ARG(F >= 0 && D >= 0 && J >= 0, "bad dims");
   if (F == 0 || J == 0) return FMX_OK;
   int64_t n = J * F;
+  if (n <= 4096 && D >= 512) {   // few long summaries: a block per (job, factor)
+    k_ic_window_blk<<<(unsigned)n, 256, 0, as_stream(stream)>>>(daily, F, D, d0_dev, d1_dev, J, out);
+    FMX_LAUNCH_CHECK("k_ic_window_blk");
+    return FMX_OK;
+  }
   k_ic_window<<<(unsigned)ceil_div(n, 256), 256, 0, as_stream(stream)>>>(daily, F, D, d0_dev, d1_dev, J, out);
   FMX_LAUNCH_CHECK("k_ic_window");
   return FMX_OK;

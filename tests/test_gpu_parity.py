@@ -298,3 +298,22 @@ def test_cs_moment_row_lengths_vs_oracle(fm, A):
             with np.errstate(all="ignore"):
                 ref = ref_fn(X[f])
             assert_close(got[f].ravel(), ref.ravel(), exact=True, what=f"{op} A={A}")
+
+
+def test_full_sample_metrics_long_panel_vs_oracle(fm):
+    """D >= 512 takes the block-per-summary window kernel: full-sample metrics vs oracle."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.metrics as OM
+    rng = np.random.default_rng(21)
+    F, D, A = 5, 640, 120
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.03] = np.nan
+    X[2] = X[1]                               # duplicated factor
+    R = 0.01 * rng.standard_normal((D, A)) + 0.002 * X[0]
+    R[rng.random(R.shape) < 0.01] = np.nan
+    daily = E.ic_daily(torch.as_tensor(X, device="cuda"), torch.as_tensor(R, device="cuda"), (1,))[0]
+    summ = E.ic_window(daily, [0], [D])[0].cpu().numpy()
+    _, vals = OM.single_factor_metrics(X, R)
+    np.testing.assert_allclose(summ[:, [0, 1, 2, 3, 6]], vals[:, [0, 1, 2, 3, 6]], rtol=1e-6, atol=1e-9)
+    assert np.array_equal(summ[1], summ[2], equal_nan=True)
