@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -363,9 +364,134 @@ void parse_chunk(Chunk& c, int ncol, int dcol, int scol, int F) {
   }
 }
 
+// Python repr(float) (float_repr_style 'short', Py_DTSF_ADD_DOT_0): shortest round-trip
+// digits; fixed notation when -4 < decpt <= 16, else d[.ddd]e+XX.  pandas' to_csv writes
+// float64 cells this way (na_rep '' for NaN).
+int py_repr(double x, char* out) {
+  if (std::isnan(x)) return 0;
+  if (std::isinf(x)) {
+    const char* s = x > 0 ? "inf" : "-inf";
+    size_t n = strlen(s);
+    memcpy(out, s, n);
+    return int(n);
+  }
+  char sci[64];
+  auto r = std::to_chars(sci, sci + sizeof sci - 1, x, std::chars_format::scientific);
+  *r.ptr = 0;  // to_chars does not terminate; the exponent is read with atoi below
+  char* p = sci;
+  char* end = r.ptr;
+  char* o = out;
+  if (*p == '-') {
+    *o++ = '-';
+    ++p;
+  }
+  char dg[32];
+  int nd = 0;
+  for (; p < end && *p != 'e'; ++p)
+    if (*p != '.') dg[nd++] = *p;
+  int e10 = std::atoi(p + 1);  // x = d1.d2... * 10^e10
+  if (nd == 1 && dg[0] == '0') e10 = 0;
+  const int decpt = e10 + 1;
+  if (decpt > -4 && decpt <= 16) {
+    if (decpt <= 0) {
+      *o++ = '0';
+      *o++ = '.';
+      for (int i = 0; i < -decpt; ++i) *o++ = '0';
+      for (int i = 0; i < nd; ++i) *o++ = dg[i];
+    } else {
+      for (int i = 0; i < decpt; ++i) *o++ = i < nd ? dg[i] : '0';
+      *o++ = '.';
+      if (nd > decpt)
+        for (int i = decpt; i < nd; ++i) *o++ = dg[i];
+      else
+        *o++ = '0';
+    }
+  } else {
+    *o++ = dg[0];
+    if (nd > 1) {
+      *o++ = '.';
+      for (int i = 1; i < nd; ++i) *o++ = dg[i];
+    }
+    *o++ = 'e';
+    *o++ = e10 < 0 ? '-' : '+';
+    int ae = e10 < 0 ? -e10 : e10;
+    if (ae < 10) *o++ = '0';
+    char eb[8];
+    auto er = std::to_chars(eb, eb + 8, ae);
+    for (char* q = eb; q < er.ptr; ++q) *o++ = *q;
+  }
+  return int(o - out);
+}
+
+std::vector<std::string_view> split_lines(const char* s, int64_t n) {
+  std::vector<std::string_view> v;
+  if (!s) return v;
+  const char* p = s;
+  for (int64_t k = 0; k < n; ++k) {
+    const char* nl = strchr(p, '\n');
+    if (!nl) break;
+    v.emplace_back(p, size_t(nl - p));
+    p = nl + 1;
+  }
+  return v;
+}
+
 }  // namespace
 
 extern "C" {
+
+int fmx_format_double(double x, char* buf, int32_t cap) {
+  char tmp[64];
+  int n = py_repr(x, tmp);
+  if (!buf || cap < n + 1) return -1;
+  memcpy(buf, tmp, size_t(n));
+  buf[n] = 0;
+  return n;
+}
+
+int fmx_csv_write(const char* path, const char* header, const char* date_strs, const char* symbol_strs,
+                  const double* X, int64_t F, int64_t D, int64_t A, const uint8_t* present, int nthreads) {
+  if (!path || !header || !date_strs || (!X && F * D * A != 0) || F < 0 || D < 0 || A < 0)
+    return fail(FMX_IO_ERR_ARG, "bad argument");
+  const auto dates = split_lines(date_strs, D);
+  const auto syms = split_lines(symbol_strs, A);
+  if (int64_t(dates.size()) != D || (symbol_strs && int64_t(syms.size()) != A) || (!symbol_strs && A != 1))
+    return fail(FMX_IO_ERR_ARG, "date/symbol string counts do not match D/A");
+  FILE* fp = fopen(path, "wb");
+  if (!fp) return fail(FMX_IO_ERR_OPEN, std::string("cannot write ") + path + ": " + strerror(errno));
+  fputs(header, fp);
+  fputc('\n', fp);
+  const int nt = pick_threads(nthreads);
+  const int64_t DA = D * A;
+  const int64_t batch = std::max<int64_t>(nt, 64);  // dates formatted per round
+  std::vector<std::string> out(static_cast<size_t>(batch));
+  for (int64_t d0 = 0; d0 < D; d0 += batch) {
+    const int64_t d1 = std::min(D, d0 + batch);
+    parallel_for(nt, d1 - d0, [&](int, int64_t lo, int64_t hi) {
+      char num[64];
+      for (int64_t i = lo; i < hi; ++i) {
+        const int64_t d = d0 + i;
+        std::string& s = out[size_t(i)];
+        s.clear();
+        for (int64_t a = 0; a < A; ++a) {
+          const int64_t cell = d * A + a;
+          if (present && !present[cell]) continue;
+          s.append(dates[size_t(d)]);
+          if (symbol_strs) (s += ',').append(syms[size_t(a)]);
+          for (int64_t f = 0; f < F; ++f) {
+            s += ',';
+            s.append(num, size_t(py_repr(X[f * DA + cell], num)));
+          }
+          s += '\n';
+        }
+      }
+    });
+    for (int64_t i = 0; i < d1 - d0; ++i) fwrite(out[size_t(i)].data(), 1, out[size_t(i)].size(), fp);
+  }
+  if (fclose(fp) != 0) return fail(FMX_IO_ERR_OPEN, std::string("write failed: ") + path);
+  return FMX_IO_OK;
+}
+
 
 const char* fmx_io_last_error(void) { return g_err.c_str(); }
 

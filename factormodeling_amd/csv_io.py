@@ -27,6 +27,8 @@ from dataclasses import dataclass
 import numpy as np
 import pandas as pd
 
+from .panel import PanelIndex
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FMX_IO_LIB", os.path.join(_HERE, "libfmx_io.so"))
 
@@ -46,6 +48,8 @@ SIGNATURES = {
     "fmx_csv_int_columns": [c_vp, c_vp],
     "fmx_csv_values": [c_vp, c_vp, c_i32],
     "fmx_csv_dense": [c_vp, c_vp, c_i32],
+    "fmx_csv_write": [c_cp, c_cp, c_cp, c_cp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i32],
+    "fmx_format_double": [ctypes.c_double, c_vp, c_i32],
 }
 
 _lib = None
@@ -79,6 +83,13 @@ def parse_double(s: str) -> float | None:
     b = s.encode()
     out = ctypes.c_double()
     return out.value if load().fmx_parse_double(b, len(b), ctypes.byref(out)) else None
+
+
+def format_double(x: float) -> str:
+    """repr(float) as the writer emits it ('' for NaN, pandas' na_rep)."""
+    buf = ctypes.create_string_buffer(64)
+    n = load().fmx_format_double(float(x), buf, 64)
+    return buf.raw[:n].decode() if n > 0 else ""
 
 
 class _Csv:
@@ -188,3 +199,53 @@ def read_long_csv(path, date_col="date", symbol_col="symbol", threads=None) -> p
         col = vals[:, j]
         cols[name] = col.astype(np.int64) if ints[j] else col
     return pd.DataFrame(cols, index=index, columns=pd.Index(names, dtype=object))
+
+
+def _plain(names, what):
+    for n in names:
+        if any(c in str(n) for c in ',"\n\r'):
+            raise ValueError(f"{what} {n!r} would need CSV quoting; not supported by the native writer")
+    return [str(n) for n in names]
+
+
+def write_long_csv(obj, path, threads=None) -> None:
+    """``obj.to_csv(path)`` for the notebook's checkpoint objects (pipeline.ipynb:217,364,
+    391,420,464-466), byte-identical: a float64 DataFrame/Series indexed by a lexsorted
+    ``(date, symbol)`` MultiIndex (factors, composite factor) or by dates (factor weights).
+    Raises ValueError for anything else (no silent pandas fallback)."""
+    frame = obj.to_frame() if isinstance(obj, pd.Series) else obj
+    if isinstance(obj, pd.Series) and obj.name is None:
+        frame.columns = ["0"]
+    if not all(dt == np.float64 for dt in frame.dtypes):
+        raise ValueError("native writer handles float64 columns only")
+    cols = _plain(frame.columns, "column")
+    idx = frame.index
+    if isinstance(idx, pd.MultiIndex):
+        if idx.nlevels != 2:
+            raise ValueError("expected a (date, symbol) MultiIndex")
+        pi = PanelIndex(idx)
+        if np.any(np.diff(pi.flat) <= 0):
+            raise ValueError("rows are not in (date, symbol) order")
+        dates, syms = pi.dates, _plain(pi.symbols, "symbol")
+        D, A = pi.D, pi.A
+        X = pi.to_dense(frame.to_numpy(dtype=np.float64))
+        present = None if pi.dense else np.ascontiguousarray(pi.present_np)
+        names = [str(n) if n is not None else "" for n in idx.names]
+    else:
+        if idx.has_duplicates or not idx.is_monotonic_increasing:
+            raise ValueError("index must be unique and increasing")
+        dates, syms = idx, None
+        D, A = len(idx), 1
+        X = np.ascontiguousarray(frame.to_numpy(dtype=np.float64).T).reshape(len(cols), D, 1)
+        present = None
+        names = [str(idx.name) if idx.name is not None else ""]
+    # D date strings formatted by pandas itself (same format decision as to_csv's)
+    dstr = pd.Series(dates).to_csv(index=False, header=False).splitlines() if D else []
+    if not isinstance(dates, pd.DatetimeIndex):
+        dstr = _plain(dstr, "index value")
+    header = ",".join(names + cols)
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    _check(load().fmx_csv_write(os.fsencode(path), header.encode(), "".join(d + "\n" for d in dstr).encode(),
+                                None if syms is None else "".join(s + "\n" for s in syms).encode(),
+                                X.ctypes.data_as(c_vp), X.shape[0], D, A,
+                                None if present is None else present.ctypes.data_as(c_vp), int(threads or 0)))

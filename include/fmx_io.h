@@ -75,6 +75,17 @@ int fmx_csv_values(const fmx_csv* h, double* out, int nthreads);
  * absent; fails with FMX_IO_ERR_DUPLICATE if a (date, symbol) pair repeats. */
 int fmx_csv_dense(const fmx_csv* h, double* out, int nthreads);
 
+/* Writer for the checkpoint CSVs the notebook emits with DataFrame/Series.to_csv
+ * (pipeline.ipynb:217,364,391,420,464-466): `header` line, then one row per present
+ * (date, symbol) cell in date-major order: date string, symbol string (omitted when
+ * symbol_strs is NULL, then A must be 1), and X[f][d][a] for f < F formatted like Python
+ * repr(float) (pandas' float64 cells; NaN -> empty).  date_strs / symbol_strs hold D / A
+ * '\n'-terminated strings.  present [D][A] may be NULL (all cells). */
+int fmx_csv_write(const char* path, const char* header, const char* date_strs, const char* symbol_strs,
+                  const double* X, int64_t F, int64_t D, int64_t A, const uint8_t* present, int nthreads);
+/* repr(float) of x into buf (NUL-terminated); returns its length, -1 if cap is too small. */
+int fmx_format_double(double x, char* buf, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -165,3 +165,69 @@ def test_format_errors_are_loud(tmp_path, text, msg):
 def test_missing_file_raises(tmp_path):
     with pytest.raises(csv_io.FmxIOError, match="cannot open"):
         csv_io.read_long_csv(tmp_path / "absent.csv")
+
+
+def test_format_double_is_python_repr():
+    rng = np.random.default_rng(9)
+    vals = list(rng.standard_normal(20000) * np.exp(rng.uniform(-60, 60, 20000)))
+    vals += [0.0, -0.0, 1.0, 123.0, 1e16, 1e15, 9999999999999998.0, 1e-4, 1e-5, 0.00012, 1e22, 5e-324,
+             1.7976931348623157e308, np.inf, -np.inf, 0.1, 1 / 3, 2.5e-310, -1234.5]
+    for v in vals:
+        assert csv_io.format_double(v) == repr(float(v)), v
+    assert csv_io.format_double(np.nan) == ""
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.2])
+def test_write_long_csv_bytes_equal_to_csv(tmp_path, drop):
+    df = _long_frame(D=20, A=15, F=6, seed=4, drop=drop).drop(columns=["count"])
+    df.iloc[3, 2] = np.inf
+    df.iloc[4, 1] = 1e16
+    a, b = tmp_path / "ref.csv", tmp_path / "got.csv"
+    df.to_csv(a)
+    csv_io.write_long_csv(df, b, threads=3)
+    assert b.read_bytes() == a.read_bytes()
+    # composite factor Series and date-indexed weights (pipeline.ipynb:391,464)
+    s = df.iloc[:, 0].rename("composite_factor")
+    s.to_csv(a)
+    csv_io.write_long_csv(s, b)
+    assert b.read_bytes() == a.read_bytes()
+    w = pd.DataFrame(np.random.default_rng(1).random((12, 4)), columns=pd.Index(list("abcd"), name="factor"),
+                     index=pd.Index(pd.bdate_range("2016-01-01", periods=12), name="date"))
+    w.iloc[2] = 0.0
+    w.to_csv(a)
+    csv_io.write_long_csv(w, b)
+    assert b.read_bytes() == a.read_bytes()
+    # and it reads back through the native loader to the same frame pandas reads
+    pd.testing.assert_frame_equal(csv_io.read_long_csv(b, symbol_col=None), _ref_load(a, symbol=False),
+                                  check_exact=True)
+
+
+def test_write_long_csv_rejects_unsupported(tmp_path):
+    df = _long_frame(D=5, A=4, F=3)
+    with pytest.raises(ValueError, match="float64"):
+        csv_io.write_long_csv(df, tmp_path / "x.csv")  # int column
+    with pytest.raises(ValueError, match="order"):
+        csv_io.write_long_csv(df.drop(columns=["count"]).iloc[::-1], tmp_path / "x.csv")
+
+
+@pytest.mark.gpu
+def test_load_panel_to_hbm_feeds_the_engine(tmp_path):
+    """CSV -> pinned host -> HBM -> cs_rank / ts_mean kernels, checked against the oracle
+    on the pandas-loaded panel."""
+    import torch
+
+    import factormodeling_amd.engine as E
+    import oracle.ops as O
+    df = _long_frame(D=40, A=300, F=3, seed=6, drop=0.0).drop(columns=["count"])
+    p = tmp_path / "f.csv"
+    df.to_csv(p)
+    ref = _ref_load(p)
+    want = PanelIndex(ref.index).to_dense(ref.to_numpy(dtype=np.float64))
+    pan = csv_io.load_panel(p, device="cuda:0")
+    assert isinstance(pan.X, torch.Tensor) and pan.X.is_cuda
+    np.testing.assert_array_equal(pan.X.cpu().numpy(), want)
+    rk = E.cs_rank(pan.X).cpu().numpy()
+    mu = E.ts("mean", pan.X, 5).cpu().numpy()
+    for f in range(want.shape[0]):
+        np.testing.assert_array_equal(rk[f], O.cs_rank(want[f]))
+        np.testing.assert_array_equal(mu[f], O.ts_mean(want[f], 5))

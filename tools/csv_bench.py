@@ -58,11 +58,21 @@ def main():
     pan = csv_io.load_panel(path, threads=a.threads)
     t_panel = time.perf_counter() - t0
     assert np.array_equal(pan.X.reshape(F, -1).T, ref.to_numpy(), equal_nan=True)
-    os.remove(path)
+    t0 = time.perf_counter()
+    ref.to_csv(path + ".ref")
+    t_wref = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    csv_io.write_long_csv(ref, path + ".got", threads=a.threads)
+    t_write = time.perf_counter() - t0
+    assert open(path + ".got", "rb").read() == open(path + ".ref", "rb").read()
+    for q in (path, path + ".ref", path + ".got"):
+        os.remove(q)
     print(json.dumps({"file_mb": round(size / 2**20, 1), "dims": [D, A, F], "threads": a.threads,
                       "ref_s": round(t_ref, 3), "frame_s": round(t_frame, 3), "panel_s": round(t_panel, 3),
                       "ref_units_per_s": units / t_ref, "panel_units_per_s": units / t_panel,
-                      "panel_MBps": size / 2**20 / t_panel, "speedup_panel": t_ref / t_panel}))
+                      "panel_MBps": size / 2**20 / t_panel, "speedup_panel": t_ref / t_panel,
+                      "write_ref_s": round(t_wref, 3), "write_s": round(t_write, 3),
+                      "speedup_write": t_wref / t_write}))
 
 
 if __name__ == "__main__":
