@@ -378,3 +378,20 @@ def wcomp(X, plan, method, present=None):
     call("fmx_wcomp_combine", ptr(Nrm), ptr(pdate), ptr(ngrp), ptr(gw), KMAX, J, D, A, ptr(present), ptr(out),
          stream_ptr())
     return out
+
+
+# ----------------------------------------------------------------------------- trade list
+def trade_equal(X, pct: float, present=None):
+    """Simulation._daily_trade_list, method 'equal' (portfolio_simulation.py:96-170) on one
+    [D][A] signal panel: (per-symbol shift(1) of the day's weights [D][A], counts [D][2])."""
+    if X.dim() != 2 or X.dtype != F64 or not X.is_cuda:
+        raise _lib.FmxError("X must be a float64 [D][A] device tensor")
+    X = X.contiguous()
+    D, A = X.shape
+    _check_present(present, D, A)
+    Wraw = torch.empty_like(X)
+    Wout = torch.empty_like(X)
+    counts = torch.empty((D, 2), dtype=F64, device=X.device)
+    call("fmx_trade_equal", ptr(X), ptr(present), ptr(Wraw), ptr(Wout), ptr(counts), D, A, float(pct),
+         stream_ptr())
+    return Wout, counts
