@@ -6,9 +6,9 @@
 // k_short likewise (:158-159); the k_long largest positives get 1.0 / k_long and the
 // k_short smallest negatives -1.0 / k_short -- exactly what _normalize_legs (:250-262)
 // computes from the 1.0 / -1.0 markers, since the leg sums are the exact integers k.
-// An element's place in its leg is its count of strictly better elements plus the equal
-// ones at lower asset index; exact ties at the k-th value are resolved that way (the
-// reference uses numpy's unstable quicksort there: implementation-defined order).
+// The k-th extreme key of each leg is found by an 8-pass LDS radix select (O(A) per row);
+// elements beyond it are selected, and exact ties AT it go to the lowest asset indices
+// (the reference uses numpy's unstable quicksort there: implementation-defined order).
 // The per-symbol shift(1) (:151-152) is fmx_ts_op(DELAY, 1) over the same presence mask.
 #include <hip/hip_runtime.h>
 #include <cmath>
@@ -18,13 +18,15 @@
 namespace fmx {
 
 constexpr int SIM_BLOCK = 256;
-constexpr int SIM_PER = 4;  // elements ranked per lane per pass (LDS reads amortised)
 
 __global__ void __launch_bounds__(SIM_BLOCK)
 k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
               double* __restrict__ counts, int64_t A, double pct) {
   extern __shared__ double sx[];  // [A]
   __shared__ int s_npos, s_nneg;
+  __shared__ unsigned s_hist[512];
+  __shared__ uint64_t s_prefix[2], s_mask[2];
+  __shared__ unsigned s_krem[2];
   const int64_t d = blockIdx.x;
   const double* x = X + d * A;
   const uint8_t* p = present ? present + d * A : nullptr;
@@ -45,39 +47,73 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   const bool flat = npos == 0 || nneg == 0;
   const int kl = flat ? 0 : max((int)floor((double)npos * pct), 1);
   const int ks = flat ? 0 : max((int)floor((double)nneg * pct), 1);
-  const double wl = flat ? 0.0 : 1.0 / (double)kl;
-  const double wsh = flat ? 0.0 : -1.0 / (double)ks;
-  for (int64_t a0 = (int64_t)threadIdx.x * SIM_PER; a0 < A; a0 += (int64_t)SIM_BLOCK * SIM_PER) {
-    double v[SIM_PER];
-    int better[SIM_PER];
-#pragma unroll
-    for (int u = 0; u < SIM_PER; ++u) {
-      v[u] = a0 + u < A ? sx[a0 + u] : __builtin_nan("");
-      better[u] = 0;
-    }
-    if (!flat) {
-      // all lanes read the same sx[b]: LDS broadcast
-      for (int64_t b = 0; b < A; ++b) {
-        const double y = sx[b];
-#pragma unroll
-        for (int u = 0; u < SIM_PER; ++u) {
-          const bool tie_before = (y == v[u]) && (b < a0 + u);
-          better[u] += (v[u] > 0.0) ? ((y > v[u]) | tie_before) : ((y < v[u]) | tie_before);
+  // pct > 1: iloc[:k] keeps the whole leg, and the leg then sums to its size
+  const int nl = min(kl, npos), ns = min(ks, nneg);
+  const double wl = flat ? 0.0 : 1.0 / (double)nl;
+  const double wsh = flat ? 0.0 : -1.0 / (double)ns;
+  if (threadIdx.x == 0) {
+    s_prefix[0] = s_prefix[1] = 0;
+    s_mask[0] = s_mask[1] = 0;
+    s_krem[0] = (unsigned)nl;
+    s_krem[1] = (unsigned)ns;
+  }
+  __syncthreads();
+  // k-th extreme of each leg by an 8-pass radix select over the 64-bit keys (positive
+  // doubles order like their bit patterns): leg 0 keys = bits(v) for v > 0, leg 1 keys =
+  // bits(-v) for v < 0; both legs want their k-th LARGEST key.
+  if (!flat) {
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = 56 - 8 * pass;
+      for (int i = threadIdx.x; i < 512; i += SIM_BLOCK) s_hist[i] = 0;
+      __syncthreads();
+      const uint64_t m0 = s_mask[0], m1 = s_mask[1], p0 = s_prefix[0], p1 = s_prefix[1];
+      for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
+        const double v = sx[a];
+        if (v > 0.0) {
+          const uint64_t k = (uint64_t)__double_as_longlong(v);
+          if ((k & m0) == p0) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
+        } else if (v < 0.0) {
+          const uint64_t k = (uint64_t)__double_as_longlong(-v);
+          if ((k & m1) == p1) atomicAdd(&s_hist[256 + ((k >> shift) & 255)], 1u);
         }
       }
+      __syncthreads();
+      if (threadIdx.x < 2) {  // one lane per leg walks its bins from the top
+        const int leg = threadIdx.x;
+        const unsigned* h = s_hist + 256 * leg;
+        unsigned cum = 0, need = s_krem[leg];
+        int bin = 255;
+        for (; bin > 0; --bin) {
+          if (cum + h[bin] >= need) break;
+          cum += h[bin];
+        }
+        s_krem[leg] = need - cum;
+        s_prefix[leg] |= (uint64_t)bin << shift;
+        s_mask[leg] |= (uint64_t)255 << shift;
+      }
+      __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < SIM_PER; ++u) {
-      const int64_t a = a0 + u;
-      if (a >= A) break;
-      double out;
-      if (p && !p[a]) out = __builtin_nan("");
-      else if (flat) out = 0.0;
-      else if (v[u] > 0.0 && better[u] < kl) out = wl;
-      else if (v[u] < 0.0 && better[u] < ks) out = wsh;
-      else out = 0.0;
-      w[a] = out;
+  }
+  const uint64_t t0 = s_prefix[0], t1 = s_prefix[1];
+  const unsigned r0 = s_krem[0], r1 = s_krem[1];
+  for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
+    const double v = sx[a];
+    double out = 0.0;
+    if (p && !p[a]) {
+      out = __builtin_nan("");
+    } else if (!flat && (v > 0.0 || v < 0.0)) {
+      const bool lg = v > 0.0;
+      const uint64_t k = (uint64_t)__double_as_longlong(lg ? v : -v);
+      const uint64_t t = lg ? t0 : t1;
+      bool sel = k > t;
+      if (k == t) {  // exact tie at the k-th key: lowest asset indices first
+        unsigned before = 0;
+        for (int64_t b = 0; b < a; ++b) before += (sx[b] == v);
+        sel = before < (lg ? r0 : r1);
+      }
+      if (sel) out = lg ? wl : wsh;
     }
+    w[a] = out;
   }
   if (threadIdx.x == 0) {
     counts[2 * d] = (double)kl;

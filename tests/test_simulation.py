@@ -67,7 +67,8 @@ def test_trade_equal_kernel_matches_golden(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("D,A,pct,ragged", [(40, 5000, 0.1, False), (30, 10000, 0.05, True),
-                                            (12, 3, 0.5, False), (8, 16384, 0.1, False)])
+                                            (12, 3, 0.5, False), (8, 16384, 0.1, False),
+                                            (10, 50, 1.5, False)])
 def test_trade_equal_kernel_matches_oracle(D, A, pct, ragged):
     import torch
 
@@ -77,6 +78,7 @@ def test_trade_equal_kernel_matches_oracle(D, A, pct, ragged):
     X[rng.random(X.shape) < 0.02] = np.nan
     X[rng.random(X.shape) < 0.02] = 0.0
     X[2] = np.abs(X[2])  # flat day
+    X[3, : A // 2] = np.round(X[3, : A // 2], 1)  # many exact ties, some at the k-th value
     present = rng.random((D, A)) >= 0.1 if ragged else np.ones((D, A), dtype=bool)
     dev = torch.device("cuda", 0)
     pres = torch.as_tensor(present.astype(np.uint8), device=dev) if ragged else None
