@@ -9,7 +9,8 @@
 // The k-th extreme key of each leg is found by an 8-pass LDS radix select (O(A) per row);
 // elements beyond it are selected, and exact ties AT it go to the lowest asset indices
 // (the reference uses numpy's unstable quicksort there: implementation-defined order).
-// The per-symbol shift(1) (:151-152) is fmx_ts_op(DELAY, 1) over the same presence mask.
+// The per-symbol shift(1) (:151-152): on a dense panel the kernel also writes each row into
+// the next date's row of Wout; with a presence mask it is fmx_ts_op(DELAY, 1) over the mask.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include "../../include/fmx.h"
@@ -21,7 +22,7 @@ constexpr int SIM_BLOCK = 256;
 
 __global__ void __launch_bounds__(SIM_BLOCK)
 k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
-              double* __restrict__ counts, int64_t A, double pct) {
+              double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double pct) {
   extern __shared__ double sx[];  // [A]
   __shared__ int s_npos, s_nneg;
   __shared__ unsigned s_hist[512];
@@ -78,18 +79,34 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
         }
       }
       __syncthreads();
-      if (threadIdx.x < 2) {  // one lane per leg walks its bins from the top
-        const int leg = threadIdx.x;
-        const unsigned* h = s_hist + 256 * leg;
-        unsigned cum = 0, need = s_krem[leg];
-        int bin = 255;
-        for (; bin > 0; --bin) {
-          if (cum + h[bin] >= need) break;
-          cum += h[bin];
+      if (threadIdx.x < 128) {  // wave w walks leg w's bins from the top, 4 bins per lane
+        const int leg = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const unsigned* h = s_hist + 256 * leg + 252 - 4 * lane;  // bins 255-4l .. 252-4l
+        const unsigned c3 = h[3], c2 = h[2], c1 = h[1], c0 = h[0];
+        const unsigned mine = c3 + c2 + c1 + c0;
+        unsigned incl = mine;  // inclusive prefix over lanes (lane 0 = top bins)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned o = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += o;
         }
-        s_krem[leg] = need - cum;
-        s_prefix[leg] |= (uint64_t)bin << shift;
-        s_mask[leg] |= (uint64_t)255 << shift;
+        const unsigned need = s_krem[leg];
+        const uint64_t hit = __ballot(incl >= need);
+        const int first = hit ? __ffsll((unsigned long long)hit) - 1 : 63;
+        if (lane == first) {
+          unsigned cum = incl - mine;
+          int bin = 255 - 4 * lane;
+          const unsigned cs[4] = {c3, c2, c1, c0};
+          int j = 0;
+          for (; j < 3; ++j) {
+            if (cum + cs[j] >= need) break;
+            cum += cs[j];
+          }
+          bin -= j;
+          s_krem[leg] = need - cum;
+          s_prefix[leg] |= (uint64_t)bin << shift;
+          s_mask[leg] |= (uint64_t)255 << shift;
+        }
       }
       __syncthreads();
     }
@@ -114,6 +131,10 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
       if (sel) out = lg ? wl : wsh;
     }
     w[a] = out;
+    if (Wshift) {  // dense panel: shift(1) per symbol is the next date's row
+      if (d + 1 < D) Wshift[(d + 1) * A + a] = out;
+      if (d == 0) Wshift[a] = __builtin_nan("");
+    }
   }
   if (threadIdx.x == 0) {
     counts[2 * d] = (double)kl;
@@ -135,8 +156,10 @@ extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, d
   const size_t lds = (size_t)A * sizeof(double);
   if (lds > 64 * 1024)
     FMX_HIP(hipFuncSetAttribute((const void*)k_trade_equal, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  k_trade_equal<<<(unsigned)D, SIM_BLOCK, lds, as_stream(stream)>>>(X, present, Wraw,
-                                                                                           counts, A, pct);
+  // dense: the kernel writes the shifted book too; ragged: shift over each symbol's rows
+  k_trade_equal<<<(unsigned)D, SIM_BLOCK, lds, as_stream(stream)>>>(X, present, Wraw, present ? nullptr : Wout,
+                                                                    counts, D, A, pct);
   FMX_LAUNCH_CHECK("k_trade_equal");
+  if (!present) return FMX_OK;
   return fmx_ts_op(FMX_TS_DELAY, Wraw, Wout, 1, D, A, A, 1, present, stream);
 }
