@@ -13,6 +13,7 @@
 // the next date's row of Wout; with a presence mask it is fmx_ts_op(DELAY, 1) over the mask.
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <algorithm>
 #include "../../include/fmx.h"
 #include "fmx_common.hpp"
 
@@ -24,7 +25,7 @@ __global__ void __launch_bounds__(SIM_BLOCK)
 k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
               double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double pct) {
   extern __shared__ double sx[];  // [A]
-  __shared__ int s_npos, s_nneg;
+  __shared__ int s_npos, s_nneg, s_npres;
   __shared__ unsigned s_hist[512];
   __shared__ uint64_t s_prefix[2], s_mask[2];
   __shared__ unsigned s_krem[2];
@@ -32,17 +33,20 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   const double* x = X + d * A;
   const uint8_t* p = present ? present + d * A : nullptr;
   double* w = W + d * A;
-  if (threadIdx.x == 0) { s_npos = 0; s_nneg = 0; }
+  if (threadIdx.x == 0) { s_npos = 0; s_nneg = 0; s_npres = 0; }
   __syncthreads();
-  int np = 0, nn = 0;
+  int np = 0, nn = 0, npr = 0;
   for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
-    const double v = (!p || p[a]) ? x[a] : __builtin_nan("");
+    const bool pr = !p || p[a];
+    npr += pr;
+    const double v = pr ? x[a] : __builtin_nan("");
     sx[a] = v;
     np += v > 0.0;
     nn += v < 0.0;
   }
   atomicAdd(&s_npos, np);
   atomicAdd(&s_nneg, nn);
+  atomicAdd(&s_npres, npr);
   __syncthreads();
   const int npos = s_npos, nneg = s_nneg;
   const bool flat = npos == 0 || nneg == 0;
@@ -136,9 +140,42 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
       if (d == 0) Wshift[a] = __builtin_nan("");
     }
   }
-  if (threadIdx.x == 0) {
-    counts[2 * d] = (double)kl;
-    counts[2 * d + 1] = (double)ks;
+  if (threadIdx.x == 0) {  // a date with no rows has no counts row in the reference: NaN
+    counts[2 * d] = s_npres ? (double)kl : __builtin_nan("");
+    counts[2 * d + 1] = s_npres ? (double)ks : __builtin_nan("");
+  }
+}
+
+// multi_manager.compute_multimanager_weights (multi_manager.py:32-81): per weight date j
+// (date index wdate[j]) and asset a, fold the manager books in factor_weights column order:
+// acc = 0.0; acc += Wf[f][d][a] * fw[j][c] for columns with a manager (colmap >= 0), a
+// nonzero weight and rows on that date (counts not NaN), NaN products filled with 0
+// (Series.add(fill_value=0), :63); counts fold fw * count likewise (:64-65).
+__global__ void k_mm_combine(const double* __restrict__ Wf, const double* __restrict__ cnt,
+                             const double* __restrict__ fw, const int32_t* __restrict__ colmap,
+                             const int32_t* __restrict__ wdate, double* __restrict__ out,
+                             double* __restrict__ out_counts, int64_t Fw, int64_t D, int64_t A) {
+  const int64_t j = blockIdx.y;
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t d = wdate[j];
+  double acc = 0.0, lc = 0.0, sc = 0.0;
+  for (int64_t c = 0; d >= 0 && c < Fw; ++c) {  // d < 0: a date no manager has
+    const int f = colmap[c];
+    const double w = fw[j * Fw + c];
+    if (f < 0 || w == 0.0) continue;
+    const double k0 = cnt[((int64_t)f * D + d) * 2];
+    if (k0 != k0) continue;  // xs(date) KeyError: manager has no rows that day
+    if (a < A) {
+      const double p = Wf[((int64_t)f * D + d) * A + a] * w;
+      if (p == p) acc = acc + p;
+    }
+    lc = lc + w * k0;
+    sc = sc + w * cnt[((int64_t)f * D + d) * 2 + 1];
+  }
+  if (a < A) out[j * A + a] = acc;
+  if (a == 0) {
+    out_counts[2 * j] = lc;
+    out_counts[2 * j + 1] = sc;
   }
 }
 
@@ -162,4 +199,17 @@ extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, d
   FMX_LAUNCH_CHECK("k_trade_equal");
   if (!present) return FMX_OK;
   return fmx_ts_op(FMX_TS_DELAY, Wraw, Wout, 1, D, A, A, 1, present, stream);
+}
+
+extern "C" fmx_status fmx_mm_combine(const double* Wf, const double* counts, const double* fw, const int32_t* colmap,
+                                     const int32_t* wdate, double* out, double* out_counts, int64_t Fw, int64_t Dw,
+                                     int64_t D, int64_t A, void* stream) {
+  FMX_ARG(Wf && counts && fw && colmap && wdate && out && out_counts && Fw >= 0 && Dw >= 0 && D >= 0 && A >= 0,
+          "bad args");
+  if (Dw == 0) return FMX_OK;
+  FMX_ARG(Dw <= 65535, "at most 65535 weight dates per call");
+  dim3 grid((unsigned)ceil_div(std::max<int64_t>(A, 1), 256), (unsigned)Dw);
+  k_mm_combine<<<grid, 256, 0, as_stream(stream)>>>(Wf, counts, fw, colmap, wdate, out, out_counts, Fw, D, A);
+  FMX_LAUNCH_CHECK("k_mm_combine");
+  return FMX_OK;
 }

@@ -395,3 +395,24 @@ def trade_equal(X, pct: float, present=None):
     call("fmx_trade_equal", ptr(X), ptr(present), ptr(Wraw), ptr(Wout), ptr(counts), D, A, float(pct),
          stream_ptr())
     return Wout, counts
+
+
+def mm_combine(Wf, counts, fw, colmap, wdate):
+    """multi_manager combination (multi_manager.py:51-72) of fmx_trade_equal outputs."""
+    F, D, A = Wf.shape
+    Dw, Fw = fw.shape
+    if tuple(counts.shape) != (F, D, 2) or len(colmap) != Fw or len(wdate) != Dw:
+        raise _lib.FmxError("mm_combine: shape mismatch")
+    cm = np.asarray(colmap, dtype=np.int32)
+    wd = np.asarray(wdate, dtype=np.int32)
+    if (cm >= F).any() or (wd >= D).any():
+        raise _lib.FmxError("mm_combine: colmap/wdate out of range")
+    dev = Wf.device
+    fw_d = torch.as_tensor(np.ascontiguousarray(fw, dtype=np.float64), device=dev)
+    cm_d = torch.as_tensor(cm, device=dev)
+    wd_d = torch.as_tensor(wd, device=dev)
+    out = torch.empty((Dw, A), dtype=F64, device=dev)
+    oc = torch.empty((Dw, 2), dtype=F64, device=dev)
+    call("fmx_mm_combine", ptr(Wf.contiguous()), ptr(counts.contiguous()), ptr(fw_d), ptr(cm_d), ptr(wd_d),
+         ptr(out), ptr(oc), Fw, Dw, D, A, stream_ptr())
+    return out, oc

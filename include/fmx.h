@@ -209,6 +209,13 @@ fmx_status fmx_wcomp_combine(const double* Nrm, const int32_t* pdate, const int3
  * (:151-152), counts [D][2] = (long_count, short_count).  A <= 16384. */
 fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
                            double* counts, int64_t D, int64_t A, double pct, void* stream);
+/* Replaces multi_manager.compute_multimanager_weights' combination loop (:51-72): Wf
+ * [F][D][A] shifted manager books and counts [F][D][2] (NaN on dates a manager has no
+ * rows) from fmx_trade_equal; fw [Dw][Fw] factor weights, colmap [Fw] column -> manager
+ * (-1: no such factor), wdate [Dw] -> date index.  out [Dw][A], out_counts [Dw][2]. */
+fmx_status fmx_mm_combine(const double* Wf, const double* counts, const double* fw, const int32_t* colmap,
+                          const int32_t* wdate, double* out, double* out_counts, int64_t Fw, int64_t Dw,
+                          int64_t D, int64_t A, void* stream);
 
 #ifdef __cplusplus
 }
