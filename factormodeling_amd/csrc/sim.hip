@@ -10,7 +10,7 @@
 // elements beyond it are selected, and exact ties AT it go to the lowest asset indices
 // (the reference uses numpy's unstable quicksort there: implementation-defined order).
 // The per-symbol shift(1) (:151-152): on a dense panel the kernel also writes each row into
-// the next date's row of Wout; with a presence mask it is fmx_ts_op(DELAY, 1) over the mask.
+// the next date's row of Wout; with a presence mask k_shift_rows walks each symbol's rows.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <algorithm>
@@ -146,6 +146,28 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   }
 }
 
+// Per-symbol shift(1) over present rows of a same-day book W (present cells are never NaN
+// in it, absent ones always are), split into date segments of SHIFT_SEG so the grid fills
+// the chip: each (segment, asset) lane first looks back for the last present value before
+// its segment, then walks its dates.
+constexpr int SHIFT_SEG = 64;
+__global__ void k_shift_rows(const double* __restrict__ W, double* __restrict__ out, int64_t D, int64_t A) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A) return;
+  const int64_t d0 = (int64_t)blockIdx.y * SHIFT_SEG;
+  const int64_t d1 = d0 + SHIFT_SEG < D ? d0 + SHIFT_SEG : D;
+  double last = __builtin_nan("");
+  for (int64_t d = d0 - 1; d >= 0; --d) {
+    const double v = W[d * A + a];
+    if (v == v) { last = v; break; }
+  }
+  for (int64_t d = d0; d < d1; ++d) {
+    const double v = W[d * A + a];
+    out[d * A + a] = (v == v) ? last : v;
+    if (v == v) last = v;
+  }
+}
+
 // multi_manager.compute_multimanager_weights (multi_manager.py:32-81): per weight date j
 // (date index wdate[j]) and asset a, fold the manager books in factor_weights column order:
 // acc = 0.0; acc += Wf[f][d][a] * fw[j][c] for columns with a manager (colmap >= 0), a
@@ -198,7 +220,10 @@ extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, d
                                                                     counts, D, A, pct);
   FMX_LAUNCH_CHECK("k_trade_equal");
   if (!present) return FMX_OK;
-  return fmx_ts_op(FMX_TS_DELAY, Wraw, Wout, 1, D, A, A, 1, present, stream);
+  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG));
+  k_shift_rows<<<g, 256, 0, as_stream(stream)>>>(Wraw, Wout, D, A);
+  FMX_LAUNCH_CHECK("k_shift_rows");
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_mm_combine(const double* Wf, const double* counts, const double* fw, const int32_t* colmap,

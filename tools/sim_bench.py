@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--assets", type=int, default=5000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cpu-dates", type=int, default=100)
+    ap.add_argument("--managers", type=int, default=20)
     a = ap.parse_args()
     D, A = a.dates, a.assets
     rng = np.random.default_rng(0)
@@ -50,7 +51,28 @@ def main():
     t0 = time.perf_counter()
     OS.trade_equal(X[:nd], np.ones((nd, A), dtype=bool), 0.1)
     cpu_s = (time.perf_counter() - t0) * D / nd
-    print(json.dumps({"workload": "trade_equal", "dates": D, "assets": A, "gpu_ms": ms,
+    # multi-manager: K ragged manager books (presence = non-NaN) + the weighted fold over
+    # all D dates (multi_manager.py:32-81), device part only
+    K = a.managers
+    pres = torch.as_tensor((~np.isnan(X)).astype(np.uint8), device=dev)
+    fw = np.random.default_rng(1).random((D, K))
+    colmap, wdate = list(range(K)), np.arange(D)
+    Wf = torch.empty((K, D, A), dtype=torch.float64, device=dev)
+    cnt = torch.empty((K, D, 2), dtype=torch.float64, device=dev)
+
+    def mm():
+        for f in range(K):
+            Wm, cm = E.trade_equal(Xd, 0.1, present=pres)
+            Wf[f] = Wm
+            cnt[f] = cm
+        return E.mm_combine(Wf, cnt, fw, colmap, wdate)
+    mm()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mm()
+    torch.cuda.synchronize()
+    mm_ms = (time.perf_counter() - t0) * 1e3
+    print(json.dumps({"workload": "trade_equal", "mm_managers": K, "mm_ms_wall": mm_ms, "dates": D, "assets": A, "gpu_ms": ms,
                       "gpu_asset_days_per_s": D * A / (ms / 1e3),
                       "alg_GBps": D * A * 24 / (ms * 1e6),  # dense: X in, Wraw out, shifted Wout out (one kernel)
                       "cpu_port_s_scaled": cpu_s, "cpu_asset_days_per_s": D * A / cpu_s, "cpu_dates_sampled": nd}))
