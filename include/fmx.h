@@ -206,7 +206,8 @@ fmx_status fmx_wcomp_combine(const double* Nrm, const int32_t* pdate, const int3
 /* Replaces Simulation._daily_trade_list with _calculate_equal_weights (:156-170) and
  * _normalize_legs (:250-262) over one [D][A] signal panel X (present [D][A] or NULL):
  * Wraw = same-day weights (NaN on absent cells), Wout = per-symbol shift(1) of Wraw
- * (:151-152), counts [D][2] = (long_count, short_count).  A <= 16384. */
+ * over present rows (:151-152), counts [D][2] = (long_count, short_count), NaN on dates
+ * with no present row.  A <= 16384. */
 fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
                            double* counts, int64_t D, int64_t A, double pct, void* stream);
 /* Replaces multi_manager.compute_multimanager_weights' combination loop (:51-72): Wf
