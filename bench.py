@@ -81,6 +81,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-factors", type=int, default=1)
     p.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    p.add_argument("--selftest-dist", action="store_true",
+                   help="CPU/gloo check of the rank launcher only (tests/test_bench_launch.py)")
     return p.parse_args()
 
 
@@ -112,9 +114,46 @@ def cpu_baseline(D, A, seed=0):
                   f"scaled to {Ds}); window metrics/selection/Gram not included")
 
 
+def spawn_ranks(n):
+    """``--gpus N`` without a torchrun launcher: start N ranks of this script as child
+    processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, one GPU each) before anything in
+    this process touches the GPU, and exit with the worst child status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.selftest_dist:
+        rank = int(os.environ.get("RANK", "0"))
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.tensor([float(rank + 1)])
+            dist.all_reduce(t)
+            world_seen = dist.get_world_size()
+            dist.destroy_process_group()
+        else:
+            t, world_seen = torch.tensor([1.0]), 1
+        if rank == 0:
+            print(json.dumps({"n_gpus": world_seen, "rank_sum": float(t.item())}))
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -89,9 +89,18 @@ class ShardedPanel:
         self.d_hi = min(D, (rank + 1) * per)
         self.halo = halo if rank > 0 else 0
         self.device = device
-        X, R, lo = synthetic_panel(D, A, F, device, seed, self.d_lo, self.d_hi, self.halo)
-        assert lo == self.d_lo - self.halo
-        self.X, self.R = X, R
+        Xo, Ro, lo = synthetic_panel(D, A, F, device, seed, self.d_lo, self.d_hi, 0)
+        assert lo == self.d_lo
+        if self.halo:
+            # halo rows start as NaN: only exchange_halo() fills them (a skipped exchange
+            # shows up as NaN rolling outputs on the first owned dates)
+            self.X = torch.full((F, self.halo + Xo.shape[1], A), float("nan"), dtype=Xo.dtype, device=device)
+            self.R = torch.full((self.halo + Ro.shape[0], A), float("nan"), dtype=Ro.dtype, device=device)
+            self.X[:, self.halo:] = Xo
+            self.R[self.halo:] = Ro
+            del Xo, Ro
+        else:
+            self.X, self.R = Xo, Ro
         self.own = self.d_hi - self.d_lo
 
     def exchange_halo(self):
@@ -230,8 +239,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
         G, N = be.gram(Z, M)
     if sp.world > 1:
-        dist.all_reduce(G)
-        dist.all_reduce(N)
+        G, N = ordered_sum(G, sp.world), ordered_sum(N, sp.world)
     C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
     _rec(timers, "gram", t0)
     t0 = _ev(timers)
@@ -242,6 +250,18 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if collect is not None:
         collect.update(daily=full, summ=summ, win=win, C=C)
     return w, kept
+
+
+def ordered_sum(T, world):
+    """Sum of every rank's ``T`` in rank order (all-gather + sequential adds), so the Gram
+    that feeds the discrete pruning decision is bitwise identical on every rank and from
+    run to run (an RCCL all-reduce leaves the summation order to the ring/tree)."""
+    parts = [torch.empty_like(T) for _ in range(world)]
+    dist.all_gather(parts, T.contiguous())
+    acc = parts[0].clone()
+    for p in parts[1:]:
+        acc += p
+    return acc
 
 
 def _ev_ok():
