@@ -144,6 +144,24 @@ def momentum(order, fret_win, max_weight=1.0, **kw):
     return np.zeros(len(order))
 
 
+def corr_prune(order, vals, Xw, rho=0.7, top_x=5, icir_threshold=-np.inf, use_rank_icir=True, **kw):
+    """Builder-defined corr_prune plugin (parity unpinned by the reference):
+    factors in metrics order above ``icir_threshold``, greedy-pruned on the correlation of
+    the window's per-date z-scored (lag-1) exposures, equal weights.  Weights aligned to
+    ``order``."""
+    from . import gram
+    col = 3 if use_rank_icir else 1
+    C = gram.corr_matrix(Xw[order])
+    v = vals[order, col]
+    with np.errstate(invalid="ignore"):
+        cand = [i for i in range(len(order)) if v[i] > icir_threshold]
+    kept = gram.greedy_prune(C, cand, rho, top_x)
+    w = np.zeros(len(order))
+    if kept:
+        w[kept] = 1.0 / len(kept)
+    return w
+
+
 def factor_selector(X, R, FR, fr_dates_mask, window, method, method_kwargs=None, present=None):
     """factor_selector.py:76-139 on a panel whose date axis is the full sorted date
     list.  ``fr_dates_mask[d]`` says whether date d is in factor_ret_df's index.
@@ -169,6 +187,8 @@ def factor_selector(X, R, FR, fr_dates_mask, window, method, method_kwargs=None,
             w = icir_top(order, vals, **kw)
         elif method == "momentum":
             w = momentum(order, FR[wd], **kw)
+        elif method == "corr_prune":
+            w = corr_prune(order, vals, Xw, **kw)
         else:
             raise ValueError(f"Unknown factor selection method: {method}")
         if cols is None:

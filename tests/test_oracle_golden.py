@@ -117,3 +117,58 @@ def test_ts_corr_vs_pandas():
     for w in (3, 5, 20):
         out = O.ts_corr(x, y, w)
         assert_close(gather(out, st, f"out_ts_corr_{w}"), st[f"out_ts_corr_{w}__v"], exact=True, what=f"ts_corr_{w}")
+
+
+# ------------------------------------------------ ragged / non-contiguous (make_golden_ragged.py)
+def test_single_factor_metrics_ragged_vs_reference():
+    st = load("metrics_ragged.npz")
+    X = np.moveaxis(st["X"], 2, 0)
+    order, vals = OM.single_factor_metrics(X, st["R"], present=st["present"])
+    names = list(st["names"])
+    canon = dup_canon(X, names)
+    assert [canon[names[k]] for k in order] == [canon[n] for n in st["out_order"]]
+    assert_close(vals[order], st["out_vals"], rtol=1e-9, atol=1e-12, what="metrics_ragged")
+
+
+def _selector_cases(prefix):
+    import json, os
+    from golden_io import GOLDEN
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    return [c for c in man["files"]["selector_ragged.npz"]["cases"] if c["key"].startswith(prefix)]
+
+
+@pytest.mark.parametrize("prefix", ["ragged_", "gap_"])
+def test_factor_selector_ragged_vs_reference(prefix):
+    st = load("selector_ragged.npz")
+    names = list(st["names"])
+    if prefix == "ragged_":
+        X, R, pres, FR = np.moveaxis(st["X"], 2, 0), st["R"], st["present"], st["FR"]
+        mask = np.ones(X.shape[1], bool)
+        dates = list(st["dates"])
+    else:
+        X, R, pres = np.moveaxis(st["gap_X"], 2, 0), st["gap_R"], None
+        mask = st["gap_fr_mask"]
+        FR = np.full((X.shape[1], X.shape[0]), np.nan)
+        FR[mask] = st["gap_FR"]
+        dates = list(st["gap_dates"])
+    canon = dup_canon(X, names)
+    for case in _selector_cases(prefix):
+        key = case["key"]
+        rows, cols, W = OM.factor_selector(X, R, FR, mask, case["window"], case["method"], case["kwargs"],
+                                           present=pres)
+        assert [str(dates[r]) for r in rows] == list(st[f"out_{key}__dates"]), key
+        ref_cols = list(st[f"out_{key}__cols"])
+        assert [canon[names[c]] for c in cols] == [canon[n] for n in ref_cols], key
+        ref = merge_dups(st[f"out_{key}__vals"], ref_cols, canon)
+        got = merge_dups(W, [names[c] for c in cols], canon)
+        assert np.array_equal(got > 0, ref > 0), key
+        assert_close(got.ravel(), ref.ravel(), rtol=1e-12, atol=0, what=key)
+
+
+def test_ts_corr_window60_vs_pandas():
+    st = load("ts_corr60_pandas.npz")
+    D, A = len(st["dates"]), len(st["syms"])
+    x, p = dense(st, "in_x", D, A)
+    y, _ = dense(st, "in_y", D, A)
+    out = O.ts_corr(x, y, 60, present=p)
+    assert_close(gather(out, st, "out_ts_corr_60"), st["out_ts_corr_60__v"], exact=True, what="ts_corr_60")
