@@ -38,6 +38,10 @@ def bytes_per_unit(stage, F):
     kind = stage.split(":")[0]
     if kind in ("ts", "cs_rank", "cs", "winsor"):
         return 16.0
+    if kind == "ts_set":            # X once + five outputs (mean, std, zscore, rank, decay)
+        return 48.0
+    if kind in ("cs_zscore_neutralize", "cs_rank_winsor"):   # X once + two outputs
+        return 24.0
     if kind == "ic_daily":
         return 8.0 + 16.0 / F
     return None
@@ -45,6 +49,8 @@ def bytes_per_unit(stage, F):
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
+                "ts_set": "fmx::k_ts_set<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
+                "cs_rank_winsor": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",
                 "cs:market_neutralize": "fmx::k_cs_moment<2>", "ts:mean": "fmx::k_ts_reg<1,",
@@ -197,6 +203,8 @@ def main():
     dom, dom_ms = max(op_stages.items(), key=lambda kv: kv[1])
     local_units = float(F) * (sp.X.shape[1]) * A
     achieved = bytes_per_unit(dom, F) * local_units / (dom_ms * 1e-3) / 1e9
+    # whole-step algorithmic bytes per unit of the HBM-priced stages (+ the Gram's X read)
+    step_bpu = sum(bytes_per_unit(k, F) for k in op_stages) + 8.0
     traffic = pmc_traffic(dom, [sp.X.shape[1], A, F]) if world == 1 else None
     if args.stages and rank == 0:
         for k, v in sorted(stages.items(), key=lambda kv: -kv[1]):
@@ -227,6 +235,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes": bytes_per_unit(dom, F) * local_units, "ms": dom_ms},
             "stages_ms": {k: round(v / args.steps, 3) for k, v in stages.items()},
+            "step_bytes_per_unit": step_bpu,
+            "step_GBs": step_bpu * local_units / (ms_step * 1e-3) / 1e9,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

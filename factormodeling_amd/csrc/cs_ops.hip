@@ -80,7 +80,8 @@ constexpr int CSM_NT = 512;
 template <int OP>
 __global__ void __launch_bounds__(CSM_NT)
 k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
-            const uint8_t* __restrict__ present, PwTable pw, double* __restrict__ stats, int slen) {
+            const uint8_t* __restrict__ present, PwTable pw, double* __restrict__ stats, int slen,
+            double* __restrict__ Y2) {
   extern __shared__ double lds[];
   __shared__ int32_t sch_l[PW_LDS_MAX];              // dense rows: the schedule for n = A
   const int64_t row = blockIdx.x;
@@ -131,6 +132,9 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
   if (stats && threadIdx.x == 0) { stats[2 * row] = mean; stats[2 * row + 1] = sd; }
   if (OP == FMX_CS_STATS_ONLY) return;
   const bool guard = (OP == FMX_CS_MARKET_NEUTRALIZE) && (sd == 0.0 || sd != sd);
+  // Y2 (cs_zscore only): market_neutralize of the same row from the same moments
+  double* y2 = (OP == FMX_CS_ZSCORE && Y2) ? Y2 + row * ld : nullptr;
+  const bool guard2 = sd == 0.0 || sd != sd;
   for (int i = threadIdx.x; i < n; i += CSM_NT) {
     double t = v[i];
     double o;
@@ -139,10 +143,11 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
     else o = (t - mean) / sd;
     int64_t a = prow ? pos[i] : i;
     y[a] = o;
+    if (y2) y2[a] = guard2 ? 0.0 : o;
   }
   if (prow) {
     for (int64_t a = threadIdx.x; a < A; a += CSM_NT)
-      if (!prow[a]) y[a] = qnan();
+      if (!prow[a]) { y[a] = qnan(); if (y2) y2[a] = qnan(); }
   }
 }
 
@@ -158,7 +163,7 @@ constexpr int CSR_EL = 16;            // elements per lane: leaves hold <= 128 =
 template <int OP>
 __global__ void __launch_bounds__(CSR_NT, 8)
 k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
-               PwTable pw, int slen, double* __restrict__ stats) {
+               PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2) {
   __shared__ int32_t sch[PW_LDS_MAX];
   __shared__ double nodes[2 * (CSR_NT / 8) + 8];
   __shared__ int iscr[CSR_NT / 64 + 2];
@@ -267,6 +272,16 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
         if (i < nfull) y[st + j + 8 * i] = outv(xv[i]);
       if (act && j == 0)
         for (int q = stop; q < len; ++q) y[st + q] = outv(x[st + q]);
+      if (OP == FMX_CS_ZSCORE && Y2) {
+        // market_neutralize of the same row from the same moments (sd in {0, NaN} -> 0)
+        const bool g2 = sd == 0.0 || sd != sd;
+        double* y2 = Y2 + row * ld;
+#pragma unroll
+        for (int i = 0; i < CSR_EL; ++i)
+          if (i < nfull) y2[st + j + 8 * i] = g2 ? 0.0 : outv(xv[i]);
+        if (act && j == 0)
+          for (int q = stop; q < len; ++q) y2[st + q] = g2 ? 0.0 : outv(x[st + q]);
+      }
     }
     __syncthreads();                                   // nodes / iscr reused by the next row
   }
@@ -637,7 +652,7 @@ static fmx_status set_lds(const void* k, size_t lds) {
 using namespace fmx;
 
 static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
-                                   const uint8_t* present, double* stats, void* stream) {
+                                   const uint8_t* present, double* stats, void* stream, double* Y2 = nullptr) {
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   fmx_status e = FMX_OK;
   PwTable pw = pw_table((int)A, &e);
@@ -680,13 +695,13 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
       const int64_t nrows = F * D;
       const int64_t grid = std::min<int64_t>(nrows, slots);
       void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
-                       (void*)&stats};
+                       (void*)&stats, (void*)&Y2};
       FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
       return FMX_OK;
     }
   }
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats,
-                  (void*)&slen};
+                  (void*)&slen, (void*)&Y2};
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(CSM_NT), args, lds, as_stream(stream)));
   return FMX_OK;
 }
@@ -706,6 +721,15 @@ extern "C" fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y
   FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_STATS, "unknown cs op");
   FMX_ARG(op == FMX_CS_STATS || Y, "null output panel");
   return cs_moment_launch(op, X, op == FMX_CS_STATS ? nullptr : Y, F, D, A, ld, present, stats, stream);
+}
+
+extern "C" fmx_status fmx_cs_zscore_neutralize(const double* X, double* Yz, double* Yn, int64_t F, int64_t D,
+                                               int64_t A, int64_t ld, const uint8_t* present, double* stats,
+                                               void* stream) {
+  FMX_ARG(X && Yz && Yn, "null panel");
+  FMX_ARG(Yz != X && Yn != X && Yz != Yn, "outputs must be distinct from X and each other");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  return cs_moment_launch(FMX_CS_ZSCORE, X, Yz, F, D, A, ld, present, stats, stream, Yn);
 }
 
 extern "C" fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
@@ -749,6 +773,20 @@ static fmx_status cs_quantile(int op, const double* X, double* Y, int64_t F, int
 extern "C" fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                                     double qlo, double qhi, const uint8_t* present, void* stream) {
   return cs_quantile(0, X, Y, F, D, A, ld, qlo, qhi, present, stream);
+}
+
+extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D,
+                                         int64_t A, int64_t ld, double qlo, double qhi, const uint8_t* present,
+                                         void* stream) {
+  FMX_ARG(X && Yrank && Ywinsor, "null panel");
+  FMX_ARG(Yrank != X && Ywinsor != X && Yrank != Ywinsor, "outputs must be distinct from X and each other");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  fmx_status e = br_cs_rank_winsor(X, Yrank, Ywinsor, F, D, A, ld, qlo, qhi, present, as_stream(stream));
+  if (e != FMX_ERR_UNSUPPORTED) return e;
+  // rows the fused kernel does not take: the two single-op passes
+  if ((e = fmx_cs_rank(X, Yrank, F, D, A, ld, FMX_RANK_AVERAGE, present, stream))) return e;
+  return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
 }
 
 extern "C" fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D, int64_t A,

@@ -9,6 +9,8 @@ namespace fmx {
 
 template <int NT, int E> constexpr auto kcr_dense = k_cs_rank_fa<NT, E, false>;
 template <int NT, int E> constexpr auto kcr_pres = k_cs_rank_fa<NT, E, true>;
+template <int NT, int E> constexpr auto kcrw_dense = k_cs_rank_fa<NT, E, false, true>;
+template <int NT, int E> constexpr auto kcrw_pres = k_cs_rank_fa<NT, E, true, true>;
 
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
                       const uint8_t* present, hipStream_t st) {
@@ -22,11 +24,33 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
     const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8;
     return launch_br(FMX_EMAX_TABLE(k_cs_rank_br), nt, A, F * D, lds, args, st);
   }
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
+  double* Y2 = nullptr;
+  double qlo = 0.0, qhi = 0.0;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(kfr, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  return FMX_OK;
+}
+
+// cs_rank (method average) and cs_winsor of the same rows in one pass (k_cs_rank_fa<WQ>);
+// returns FMX_ERR_UNSUPPORTED when the row does not fit the fine kernel (caller splits).
+fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
+                             double qlo, double qhi, const uint8_t* present, hipStream_t st) {
+  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
+  const int E = br_emax(A, nt_fa);
+  const void* k = present ? FMX_EMAX_TABLE(kcrw_pres)(nt_fa, E) : FMX_EMAX_TABLE(kcrw_dense)(nt_fa, E);
+  if (rank_impl() == RANK_IMPL_BR || E < 0 || !lds_fits(k, lds_fr)) return FMX_ERR_UNSUPPORTED;
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D == 0) return FMX_OK;
+  int method = FMX_RANK_AVERAGE;
+  void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi};
+  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;
 }
 

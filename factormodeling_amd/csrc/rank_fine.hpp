@@ -38,10 +38,15 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 // counters are read into registers after their scan, and only then are the keys of
 // shared fine buckets scattered over them.  ~42 KB per row: three rows per CU.
 // Positions t + k*NT with k < EMAX-1 are always inside the row (EMAX = ceil(A/NT)).
-template <int NT, int EMAX, bool PRES>
+//
+// WQ: also cs_winsor of the same row into Y2 (operations.py:64-68) from the same histogram.
+// The four numpy 'linear' order statistics are read off the ranks: after the in-bucket
+// scan every element knows #less / #equal among the valid keys, so the owner of order
+// statistic k (less <= k < less + equal) publishes its key -- no second pass over the row.
+template <int NT, int EMAX, bool PRES, bool WQ = false>
 __global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
-             const uint8_t* __restrict__ present) {
+             const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
@@ -103,6 +108,11 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 #pragma unroll
     for (int k = 0; k < EMAX; ++k)
       if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+    if (WQ) {                                 // nv < 5: winsor is the identity
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k)
+        if (k < EMAX - 1 || last_in) Y2[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+    }
     return;
   }
   if (wid == 0) {
@@ -159,6 +169,26 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     }
   }
   const double den = (double)(nrow - 1);
+  // winsor order statistics (numpy linear) of the nv valid keys
+  __shared__ uint64_t tval[4];
+  int kk[4] = {0, 0, 0, 0};
+  double gq[2] = {0.0, 0.0};
+  if (WQ && nv >= 5) {
+    const double qs[2] = {qlo, qhi};
+#pragma unroll
+    for (int z = 0; z < 2; ++z) {
+      const double vi = (double)(nv - 1) * qs[z];
+      if (vi >= (double)(nv - 1)) {
+        kk[2 * z] = kk[2 * z + 1] = nv - 1;
+        gq[z] = vi + 1.0;
+      } else {
+        const double pf = floor(vi);
+        kk[2 * z] = (int)pf;
+        kk[2 * z + 1] = (int)pf + 1;
+        gq[z] = vi - pf;
+      }
+    }
+  }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     if (!(k < EMAX - 1 || last_in)) continue;
@@ -169,6 +199,36 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
     y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
+    if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (less <= kk[j] && kk[j] < less + eq) tval[j] = key[k];   // all writers store the same key
+    }
+  }
+  if (WQ) {
+    __syncthreads();
+    double lo = qnan(), hi = qnan();
+    if (nv >= 5) {
+      double qv[2];
+#pragma unroll
+      for (int z = 0; z < 2; ++z) {
+        const double a = okey_inv(tval[2 * z]), b = okey_inv(tval[2 * z + 1]);
+        const double g = gq[z];
+        const double diff = b - a;
+        qv[z] = (g >= 0.5) ? b - diff * (1.0 - g) : a + diff * g;
+      }
+      lo = qv[0];
+      hi = qv[1];
+    }
+    double* y2 = Y2 + row * ld;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      if (!(k < EMAX - 1 || last_in)) continue;
+      const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+      double o = v;
+      if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
+      y2[t + k * NT] = (PRES && !((pm >> k) & 1)) ? qnan() : o;
+    }
   }
   BR_PH();
 }
@@ -363,8 +423,10 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
 // (#members | #lag-0 members << 16 | #lag-1 members << 32), so a single atomic gives the
 // scatter slot and a single scan gives both lags' rank bases.
 // Output: out[((m*4 + j) * F + f) * D + s + L_m], j = n, IC, rank IC, beta.
+// Occupancy target: two 1024-thread rows per CU (64 VGPRs) while the row's LDS allows it
+// (A <= 5120); longer rows hold one row per CU anyway (LDS), so they get 128 VGPRs.
 template <int NT, int EMAX>
-__global__ void __launch_bounds__(NT, NT == 1024 ? 8 : 4)
+__global__ void __launch_bounds__(NT, (NT == 1024 && EMAX <= 5) ? 8 : 4)
 k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64_t F, int64_t D, int64_t A,
               int64_t ld, int L0, int L1, int NL, double* __restrict__ out) {
   constexpr int K = FR_K_IC, NB = FRG<K>::NB, NW = NT / 64;
@@ -470,54 +532,60 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
     __syncthreads();
     fr_scan<NT, u64>(cnt, NB, uscr);
     BR_PH();
-    // a0[k] / a1[k] = #less | #equal << 16 among the bucket's lag-0 / lag-1 members
-    int msk[EMAX], s0[EMAX], len[EMAX], a0[EMAX], a1[EMAX];
+    // a0[k] / a1[k] = #less | #equal << 16 among the bucket's lag-0 / lag-1 members;
+    // sl[k] = bucket start | scan length << 16 (packed: the kernel runs at 64 VGPRs)
+    int sl[EMAX], a0[EMAX], a1[EMAX];
     int maxlen = 0;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      msk[k] = 0; s0[k] = 0; len[k] = 0; a0[k] = 0; a1[k] = 0;
+      sl[k] = 0; a0[k] = 0; a1[k] = 0;
       if (key[k] == KEY_SENTINEL) continue;
       const int b = (pk[k] >> PK_BSHIFT) & FR_BMASK;
-      msk[k] = pk[k] >> FR_MSH;
+      const int mk = pk[k] >> FR_MSH;
       const u64 c0 = cnt[b], dc = cnt[b + 1] - c0;
       const int nall = (int)(dc & 0xffff);
-      s0[k] = (int)(c0 & 0xffff);
+      const int s0 = (int)(c0 & 0xffff);
+      int len = 0;
       if ((b % (K + 1)) == K) {
         a0[k] = (int)((dc >> 16) & 0xffff) << 16;
         a1[k] = (int)((dc >> 32) & 0xffff) << 16;
       } else if (nall == 1) {
-        a0[k] = (msk[k] & 1) << 16;
-        a1[k] = (msk[k] >> 1) << 16;
+        a0[k] = (mk & 1) << 16;
+        a1[k] = (mk >> 1) << 16;
       } else {
-        len[k] = nall;
-        const int q = s0[k] + (pk[k] & PK_SLOT);
+        len = nall;
+        const int q = s0 + (pk[k] & PK_SLOT);
         bkey[q] = key[k];
-        bmask[q] = (uint8_t)msk[k];
+        bmask[q] = (uint8_t)mk;
       }
-      maxlen = max(maxlen, len[k]);
+      sl[k] = s0 | (len << 16);
+      maxlen = max(maxlen, len);
     }
     __syncthreads();
     BR_PH();
     for (int j = 0; j < maxlen; ++j) {
 #pragma unroll
       for (int k = 0; k < EMAX; ++k) {
-        if (j < len[k]) {
-          const uint64_t w = bkey[s0[k] + j];
-          const int wm = bmask[s0[k] + j];
+        if (j < (sl[k] >> 16)) {
+          const int q = (sl[k] & 0xffff) + j;
+          const uint64_t w = bkey[q];
+          const int wm = bmask[q];
           const int inc = (w < key[k]) + ((w == key[k]) << 16);
           a0[k] += (wm & 1) ? inc : 0;
           a1[k] += (wm & 2) ? inc : 0;
         }
       }
     }
-    // pk[k] <- 2*rank(lag 0) | 2*rank(lag 1) << 16 (half-integer ranks, exact)
+    // pk[k] <- 2*rank(lag 0) | 2*rank(lag 1) << 16 (half-integer ranks, exact); a field is
+    // 0 when the element is not a member of that lag's pairs
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       if (key[k] == KEY_SENTINEL) continue;
+      const int mk = pk[k] >> FR_MSH;
       const u64 c0 = cnt[(pk[k] >> PK_BSHIFT) & FR_BMASK];
       const int b0 = (int)((c0 >> 16) & 0xffff), b1 = (int)((c0 >> 32) & 0xffff);
-      pk[k] = (2 * (b0 + (a0[k] & 0xffff)) + (a0[k] >> 16) + 1) |
-              ((2 * (b1 + (a1[k] & 0xffff)) + (a1[k] >> 16) + 1) << 16);
+      pk[k] = ((mk & 1) ? (2 * (b0 + (a0[k] & 0xffff)) + (a0[k] >> 16) + 1) : 0) |
+              ((mk & 2) ? ((2 * (b1 + (a1[k] & 0xffff)) + (a1[k] >> 16) + 1) << 16) : 0);
     }
     double fm[2], rm[2], km[2];
 #pragma unroll
@@ -534,10 +602,10 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
       double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int k = 0; k < EMAX; ++k) {
-        if (!((msk[k] >> m) & 1)) continue;
+        const int r2 = key[k] == KEY_SENTINEL ? 0 : (m == 0 ? (pk[k] & 0xffff) : (int)((unsigned)pk[k] >> 16));
+        if (r2 == 0) continue;
         const int64_t i = t + (int64_t)k * NT;
         const double fv = okey_inv(key[k]);
-        const int r2 = m == 0 ? (pk[k] & 0xffff) : (int)((unsigned)pk[k] >> 16);
         const double rk = (double)r2 / 2.0;
         const double r = rr[m][i];
         const double dx = fv - fm[m], dy = r - rm[m], dk = rk - km[m];

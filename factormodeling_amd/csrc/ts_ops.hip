@@ -325,6 +325,123 @@ k_ts_reg(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_
   }
 }
 
+// Fused rolling set over ONE read of the panel: ts_mean(W), ts_std(W), ts_zscore(W),
+// ts_rank(WR) and ts_decay(W) with WR <= W (operations.py:10-48) -- the C2 operator set.
+// One lane per (factor, asset) column as k_ts_reg; the W-slot register ring serves all
+// five, and the mean / Welford machines are shared, exactly as the separate kernels run
+// them (ts_zscore is (v - ts_mean) / ts_std with 0 -> NaN, operations.py:18-21), so each
+// output is bit-identical to its single-op kernel.  The rank window is the newest WR
+// slots of the same ring.  A null output pointer skips that store.
+// Algorithmic bytes: 8 B read + 8 B per requested output per factor·asset·day (48 B for
+// all five, vs 80 B for five single-op passes).
+#ifndef TS_SET_WAVES
+#define TS_SET_WAVES 4
+#endif
+struct SetSt {
+  MeanSt ms;
+  VarSt vs;
+  int64_t i;
+  int nan_w, nan_r;
+  bool first;
+};
+
+template <int W, int WR>
+__device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, int q, int64_t off,
+                                            double* __restrict__ Ym, double* __restrict__ Ys,
+                                            double* __restrict__ Yz, double* __restrict__ Yr,
+                                            double* __restrict__ Yd) {
+  if (c.first) { c.ms.init(v); c.vs.init(v); c.first = false; }
+  const bool full = c.i >= W;
+  const double old = full ? ring[q] : qnan();
+  // element leaving the rank window (still in the ring when WR < W)
+  const double oldr = (WR == W) ? old : ((c.i >= WR) ? ring[(q + W - WR) % W] : qnan());
+  ring[q] = v;
+  if (full) { c.ms.remove(old); c.vs.remove(old); }
+  c.ms.add(v); c.vs.add(v);
+  const double m = c.ms.result(W);
+  const double sd = zsqrt(c.vs.var(W, 1));
+  if (Ym) Ym[off] = m;
+  if (Ys) Ys[off] = sd;
+  if (Yz) Yz[off] = (v - m) / (sd == 0.0 ? qnan() : sd);
+  if (full && old != old) c.nan_w -= 1;
+  if (c.i >= WR && oldr != oldr) c.nan_r -= 1;
+  if (v != v) { c.nan_w += 1; c.nan_r += 1; }
+  if (Yr) {
+    double o = qnan();
+    if (c.i + 1 >= WR && c.nan_r == 0) {
+      int less = 0, eq = 0;
+#pragma unroll
+      for (int k = 0; k < WR; ++k) {
+        const double w = ring[(q + W - k) % W];
+        less += (w < v);
+        eq += (w == v);
+      }
+      o = ((double)less + (double)(eq + 1) / 2.0) / (double)WR;
+    }
+    Yr[off] = o;
+  }
+  if (Yd) {
+    double o = qnan();
+    if (c.i + 1 >= W && c.nan_w == 0) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 1; k <= W; ++k) acc += ring[(q + k) % W] * (double)k;
+      o = acc / ((double)W * (double)(W + 1) / 2.0);
+    }
+    Yd[off] = o;
+  }
+  c.i += 1;
+  __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps' live ranges apart
+}
+
+template <int W, int WR, int PF>
+__global__ void __launch_bounds__(256, TS_SET_WAVES)
+k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restrict__ Ys, double* __restrict__ Yz,
+         double* __restrict__ Yr, double* __restrict__ Yd, int64_t F, int64_t D, int64_t A, int64_t ld) {
+  static_assert(W % PF == 0 && WR >= 1 && WR <= W, "windows");
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const int64_t off0 = f * D * ld + a;
+  const double* xp = X + off0;
+  SetSt c;
+  c.i = 0; c.nan_w = 0; c.nan_r = 0; c.first = true;
+  double ring[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) ring[q] = 0.0;
+  double pf[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) pf[q] = q < D ? xp[q * ld] : 0.0;
+  xp += PF * ld;
+  int64_t off = off0;
+  int64_t d0 = 0;
+  for (; d0 + W + PF <= D; d0 += W) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const double v = pf[q % PF];
+      pf[q % PF] = *xp;
+      xp += ld;
+      ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
+      off += ld;
+      asm volatile("" : "+v"(off));   // no per-step address precomputation (spills)
+    }
+  }
+  for (; d0 < D; d0 += W) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const int64_t d = d0 + q;
+      if (d < D) {
+        const double v = pf[q % PF];
+        if (d + PF < D) pf[q % PF] = *xp;
+        xp += ld;
+        ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
+        off += ld;
+      asm volatile("" : "+v"(off));   // no per-step address precomputation (spills)
+      }
+    }
+  }
+}
+
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // One lane owns V adjacent assets of one factor (V = 2: 16-byte loads/stores) and walks
@@ -634,6 +751,32 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
   }
 #undef FMX_TSK
   return launch_ring(k, grid, lds, st, args);
+}
+
+extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, double* Yzscore, double* Yrank,
+                                 double* Ydecay, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t window,
+                                 int32_t rank_window, const uint8_t* present, void* stream) {
+  FMX_ARG(X, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(window >= 1 && rank_window >= 1, "windows must be >= 1");
+  double* outs[5] = {Ymean, Ystd, Yzscore, Yrank, Ydecay};
+  for (int k = 0; k < 5; ++k) FMX_ARG(outs[k] != X, "outputs must not alias X");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  if (!present && window == 20 && rank_window == 10 && getenv("FMX_TS_SET_SPLIT") == nullptr) {
+    void* args[] = {(void*)&X, (void*)&Ymean, (void*)&Ystd, (void*)&Yzscore, (void*)&Yrank, (void*)&Ydecay,
+                    (void*)&F, (void*)&D, (void*)&A, (void*)&ld};
+    FMX_HIP(hipLaunchKernel((const void*)k_ts_set<20, 10, 5>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args,
+                            0, as_stream(stream)));
+    return FMX_OK;
+  }
+  // other windows / ragged panels: one single-op pass per requested output
+  const int32_t ops[5] = {FMX_TS_MEAN, FMX_TS_STD, FMX_TS_ZSCORE, FMX_TS_RANK, FMX_TS_DECAY};
+  for (int k = 0; k < 5; ++k) {
+    if (!outs[k]) continue;
+    fmx_status e = fmx_ts_op(ops[k], X, outs[k], F, D, A, ld, k == 3 ? rank_window : window, present, stream);
+    if (e) return e;
+  }
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* Out, int64_t F, int64_t D,

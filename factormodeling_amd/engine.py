@@ -56,6 +56,24 @@ def ts(op: str, X, window: int, present=None, out=None):
     return Y
 
 
+TS_SET = ("mean", "std", "zscore", "rank", "decay")
+
+
+def ts_set(X, outs: dict, window: int, rank_window: int, present=None):
+    """Fused rolling set (fmx_ts_set): ``outs`` maps a subset of TS_SET to output
+    tensors shaped like X; mean/std/zscore/decay use ``window``, rank ``rank_window``."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    bad = set(outs) - set(TS_SET)
+    if bad:
+        raise ValueError(f"ts_set: unsupported ops {sorted(bad)}")
+    ps = [ptr(_out(X, outs[k])) if k in outs else None for k in TS_SET]
+    call("fmx_ts_set", ptr(X), *ps, F, D, A, A, int(window), int(rank_window), ptr(present), stream_ptr())
+    return outs
+
+
 def ts_corr(X, Ycol, window: int, present=None):
     X = as3(X)
     _check_panel(X)
@@ -115,6 +133,31 @@ def cs_moment_stats(op: str, X, present=None, out=None):
     stats = torch.empty((F, D, 2), dtype=F64, device=X.device)
     call("fmx_cs_moment_stats", CS[op], ptr(X), ptr(Y), F, D, A, A, ptr(present), ptr(stats), stream_ptr())
     return Y, stats
+
+
+def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=False):
+    """cs_zscore and market_neutralize from one set of row moments (fmx_cs_zscore_neutralize).
+    Returns (Yz, Yn) or (Yz, Yn, stats[F][D][2])."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Yz, Yn = _out(X, out_z), _out(X, out_n)
+    stats = torch.empty((F, D, 2), dtype=F64, device=X.device) if with_stats else None
+    call("fmx_cs_zscore_neutralize", ptr(X), ptr(Yz), ptr(Yn), F, D, A, A, ptr(present), ptr(stats), stream_ptr())
+    return (Yz, Yn, stats) if with_stats else (Yz, Yn)
+
+
+def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None):
+    """cs_rank(average) and cs_winsor(qlo, qhi) in one pass (fmx_cs_rank_winsor)."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    Yr, Yw = _out(X, out_rank), _out(X, out_winsor)
+    call("fmx_cs_rank_winsor", ptr(X), ptr(Yr), ptr(Yw), F, D, A, A, float(qlo), float(qhi), ptr(present),
+         stream_ptr())
+    return Yr, Yw
 
 
 def cs_rank(X, method="average", present=None, out=None):

@@ -38,6 +38,42 @@ class StepConfig:
     icir_threshold: float = -1.0
     prune_rho: float = 0.7
     ops: list = field(default_factory=lambda: list(OPS))
+    fuse: bool = True          # multi-output kernels: one read of X for several operators
+
+
+def _op_key(kind, op, w):
+    return f"{kind}:{op or ''}:{w or ''}"
+
+
+def plan_ops(ops, be, fuse=True):
+    """Group the operator list into launches.  With ``fuse`` and a backend that has the
+    multi-output kernels: the rolling set {mean, std, zscore, decay at W; rank at WR}
+    becomes one ts_set pass, cs_zscore + market_neutralize one moment pass, cs_rank +
+    cs_winsor one histogram pass.  Returns [(stage_name, [(kind, op, w), ...])]."""
+    left = list(ops)
+    stages = []
+    if fuse and hasattr(be, "ts_set"):
+        ts = [o for o in left if o[0] == "ts" and o[1] in ("mean", "std", "zscore", "rank", "decay")]
+        W = {o[2] for o in ts if o[1] != "rank"}
+        WR = {o[2] for o in ts if o[1] == "rank"}
+        names = [o[1] for o in ts]
+        if len(ts) >= 2 and len(W) <= 1 and len(WR) <= 1 and len(set(names)) == len(names):
+            w = next(iter(W)) if W else next(iter(WR))
+            wr = next(iter(WR)) if WR else w
+            stages.append((f"ts_set:{w}:{wr}", ts))
+            left = [o for o in left if o not in ts]
+    if fuse and hasattr(be, "cs_zscore_neutralize"):
+        pair = [("cs", "zscore", None), ("cs", "market_neutralize", None)]
+        if all(p in left for p in pair):
+            stages.append(("cs_zscore_neutralize", pair))
+            left = [o for o in left if o not in pair]
+    if fuse and hasattr(be, "cs_rank_winsor"):
+        pair = [("cs_rank", None, None), ("winsor", None, None)]
+        if all(p in left for p in pair):
+            stages.append(("cs_rank_winsor", pair))
+            left = [o for o in left if o not in pair]
+    stages += [(_op_key(*o), [o]) for o in left]
+    return stages
 
 
 def synthetic_panel(D, A, F, device, seed=0, d_lo=0, d_hi=None, halo=0):
@@ -130,6 +166,25 @@ class ShardedPanel:
 class EngineBackend:
     """The product compute backend: libfmx kernels on the local GPU."""
 
+    @staticmethod
+    def ts_set(X, ops, outs):
+        """ops: [(kind, op, w)] of the rolling set; outs: one buffer per op."""
+        W = {w for _, op, w in ops if op != "rank"}
+        WR = {w for _, op, w in ops if op == "rank"}
+        w = next(iter(W)) if W else next(iter(WR))
+        wr = next(iter(WR)) if WR else w
+        E.ts_set(X, {op: y for (_, op, _), y in zip(ops, outs)}, w, wr)
+
+    @staticmethod
+    def cs_zscore_neutralize(X, outs):
+        """Returns cs_zscore's row stats (mean, std) for the Gram."""
+        _, _, stats = E.cs_zscore_neutralize(X, outs[0], outs[1], with_stats=True)
+        return stats
+
+    @staticmethod
+    def cs_rank_winsor(X, outs):
+        E.cs_rank_winsor(X, 0.01, 0.99, outs[0], outs[1])
+
     def op(self, kind, op, w, X, out):
         if kind == "ts":
             return E.ts(op, X, w, None, out=out)
@@ -167,21 +222,39 @@ class EngineBackend:
 ENGINE = EngineBackend()
 
 
-def run_ops(X, cfg: StepConfig, out=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None):
-    """Operator set over the local panel (halo rows included as warm-up).  ``collect``
+def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None):
+    """Operator set over the local panel (halo rows included as warm-up), as planned by
+    ``plan_ops``; every operator writes its own output buffer (``bufs``: a list of tensors
+    shaped like X, reused across steps; as many as the widest fused launch).  ``collect``
     (a dict) receives a copy of every operator's owned-date output (tests only); ``side``
     (a dict) receives by-products later stages reuse (cs_zscore's row stats)."""
-    Y = out if out is not None else torch.empty_like(X)
-    for kind, op, w in cfg.ops:
+    stages = plan_ops(cfg.ops, be, cfg.fuse)
+    need = max(len(o) for _, o in stages)
+    bufs = list(bufs or [])
+    while len(bufs) < need:
+        bufs.append(torch.empty_like(X))
+    for name, ops in stages:
+        outs = bufs[:len(ops)]
         t0 = _ev(timers)
-        if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
-            _, side["stats"] = be.cs_zscore_stats(X, Y)
+        if name.startswith("ts_set:"):
+            be.ts_set(X, ops, outs)
+        elif name == "cs_zscore_neutralize":
+            st = be.cs_zscore_neutralize(X, outs)
+            if side is not None:
+                side["stats"] = st
+        elif name == "cs_rank_winsor":
+            be.cs_rank_winsor(X, outs)
         else:
-            be.op(kind, op, w, X, Y)
-        _rec(timers, f"{kind}:{op or ''}:{w or ''}", t0)
+            kind, op, w = ops[0]
+            if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
+                _, side["stats"] = be.cs_zscore_stats(X, outs[0])
+            else:
+                be.op(kind, op, w, X, outs[0])
+        _rec(timers, name, t0)
         if collect is not None:
-            collect[f"{kind}:{op or ''}:{w or ''}"] = Y[:, own].clone()
-    return Y
+            for o, y in zip(ops, outs):
+                collect[_op_key(*o)] = y[:, own].clone()
+    return bufs
 
 
 def _ev(timers):
@@ -207,7 +280,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     sp.exchange_halo()
     _rec(timers, "halo", t0)
     side = {}
-    run_ops(sp.X, cfg, timers=timers, be=be, collect=collect, own=slice(sp.halo, None), side=side)
+    sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                      own=slice(sp.halo, None), side=side)
     # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     daily = be.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]

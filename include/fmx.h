@@ -101,6 +101,15 @@ fmx_status fmx_device_info(char* buf, int64_t buflen);
 fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                      int32_t window, const uint8_t* present, void* stream);
 
+/* Fused rolling set: ts_mean(window), ts_std(window), ts_zscore(window), ts_rank(rank_window)
+ * and ts_decay(window) (operations.py:10-48) from ONE read of X.  Any output may be NULL
+ * (not computed); none may alias X.  Each output is bit-identical to fmx_ts_op of that op.
+ * Dense panels with (window, rank_window) = (20, 10) run one fused kernel; other windows
+ * and ragged panels run one fmx_ts_op pass per requested output. */
+fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, double* Yzscore, double* Yrank, double* Ydecay,
+                      int64_t F, int64_t D, int64_t A, int64_t ld, int32_t window, int32_t rank_window,
+                      const uint8_t* present, void* stream);
+
 /* Builder-defined ts_corr (no reference counterpart): per-symbol rolling Pearson of X[f]
  * against Ycol (y_fstride = 0: one [D][ld] series shared by all factors, e.g. returns),
  * pandas Rolling.corr semantics, min_periods = window. */
@@ -121,9 +130,21 @@ fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int6
  * only the stats (Y may be NULL); they feed fmx_gram_fused. */
 fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                                const uint8_t* present, double* stats, void* stream);
+
+/* cs_zscore (Yz) and market_neutralize (Yn) of the same rows from ONE set of moments
+ * (operations.py:77-78, :171-182); optional stats[F][D][2] = (mean, std ddof=0).  Outputs
+ * bit-identical to fmx_cs_moment of each op; distinct from X and each other. */
+fmx_status fmx_cs_zscore_neutralize(const double* X, double* Yz, double* Yn, int64_t F, int64_t D, int64_t A,
+                                    int64_t ld, const uint8_t* present, double* stats, void* stream);
 /* cs_rank (operations.py:54-62): (rank - 1) / (rows - 1), rows counting NaN. */
 fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
                        const uint8_t* present, void* stream);
+
+/* cs_rank(method='average') and cs_winsor(limits=(qlo, qhi)) of the same rows in ONE pass
+ * (operations.py:54-68): the winsor quantiles' order statistics are read off the rank
+ * histogram.  Outputs bit-identical to fmx_cs_rank / fmx_cs_winsor; distinct from X. */
+fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
+                              int64_t ld, double qlo, double qhi, const uint8_t* present, void* stream);
 /* cs_winsor (operations.py:64-68); qlo/qhi are the fractions numpy sees
  * (pandas passes q*100 and numpy divides by 100). */
 fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, double qlo,

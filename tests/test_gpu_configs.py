@@ -49,7 +49,7 @@ def test_step_engine_vs_oracle(dev):
     w_g, kept_g = PL.run_step(sp, cfg, collect=col_g)
     torch.cuda.synchronize()
     spc = copy.copy(sp)
-    spc.X, spc.R = sp.X.cpu(), sp.R.cpu()
+    spc.X, spc.R, spc.bufs = sp.X.cpu(), sp.R.cpu(), None
     col_o = {}
     w_o, kept_o = PL.run_step(spc, cfg, be=OracleBackend(), collect=col_o)
     for kind, op, w in cfg.ops:

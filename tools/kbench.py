@@ -53,6 +53,15 @@ def panel(D, A, F, seed=0, block=8):
     return X, torch.as_tensor(r, device="cuda")
 
 
+_SET = {}
+
+
+def _set_outs(X):
+    if not _SET:
+        _SET.update({k: torch.empty_like(X) for k in E.TS_SET})
+    return _SET
+
+
 OPS = {
     "ts_mean": (lambda X, R, Y: E.ts("mean", X, 20, out=Y), 16),
     "ts_std": (lambda X, R, Y: E.ts("std", X, 20, out=Y), 16),
@@ -64,6 +73,7 @@ OPS = {
     "market_neutralize": (lambda X, R, Y: E.cs_moment("market_neutralize", X, out=Y), 16),
     "winsor": (lambda X, R, Y: E.cs_quantile_op("winsor", X, 0.01, 0.99, out=Y), 16),
     "ic": (lambda X, R, Y: E.ic_daily(X, R, (1, 2)), 8),
+    "ts_set": (lambda X, R, Y: E.ts_set(X, _set_outs(X), 20, 10), 48),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
     "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
     "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
