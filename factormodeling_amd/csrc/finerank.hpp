@@ -116,6 +116,13 @@ __device__ __forceinline__ double fr_wave_sum_d(double v) {
   v = fr_row_sum_d(v);
   return (fr_readlane_d(v, 0) + fr_readlane_d(v, 16)) + (fr_readlane_d(v, 32) + fr_readlane_d(v, 48));
 }
+// A block-uniform double moved to SGPRs (frees two VGPRs for the rest of the kernel).
+__device__ __forceinline__ double fr_uniform_d(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ uint64_t fr_readlane_u64(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);

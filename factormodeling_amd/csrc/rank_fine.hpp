@@ -435,11 +435,16 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   static_assert(NB <= FR_BMASK, "bucket id field");
   using u64 = unsigned long long;
   __shared__ FrTab tab;
-  __shared__ u64 cnt[NB + 1];
   __shared__ u64 uscr[NW];
   __shared__ double dscr[(NW + 1) * 16];
-  extern __shared__ uint64_t bkey[];          // A keys, then A mask bytes
-  uint8_t* bmask = (uint8_t*)(bkey + A);
+  // one dynamic buffer, two lives: the NB+1 packed bucket counters, then (once every
+  // element has read its counters) the bucket-ordered keys [A], member info [A] and lag
+  // masks [A] of the in-bucket scan
+  extern __shared__ uint64_t lds[];
+  u64* cnt = (u64*)lds;
+  uint64_t* bkey = lds;
+  uint32_t* binfo = (uint32_t*)(bkey + A);    // bucket start | member count << 16 (0: no scan)
+  uint8_t* bmask = (uint8_t*)(binfo + A);
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
   // date-major rows: the F workgroups of a date share its return rows in L2 (measured
@@ -457,11 +462,13 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   if (!act[0] && !act[1]) return;
   uint64_t key[EMAX];
   int pk[EMAX];                               // mask << FR_MSH, later slot | bucket
-  // v1: n per lag, sum f per lag, sum r per lag;  mx: -min f, max f, -min r, max r per lag
-  double v1[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // [6, 8): butterfly padding
+  // v1: sum f, sum r of lag 0, then of lag 1 (pair counts come from ballots);
+  // mx: -min f, max f, -min r, max r per lag
+  double v1[4] = {0, 0, 0, 0};
   double mx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
+  int cw0 = 0, cw1 = 0;                       // wave-uniform pair counts per lag
   // the row's exposures are all in flight before the first is consumed
   const bool last_in = t + (EMAX - 1) * NT < A;
   double xv[EMAX];
@@ -472,44 +479,51 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
     const int i = t + k * NT;
     key[k] = KEY_SENTINEL;
     pk[k] = 0;
-    {
-      const double v = xv[k];
-      if (v == v) {
-        int mm = 0;
+    int mm = 0;
+    const double v = xv[k];
+    if (v == v) {
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          if (!act[m]) continue;
-          const double r = rr[m][i];
-          if (r != r) continue;
-          mm |= 1 << m;
-          v1[m] += 1.0;
-          v1[2 + 2 * m] += v;
-          v1[3 + 2 * m] += r;
-          mx[4 * m + 0] = fmax(mx[4 * m + 0], -v);
-          mx[4 * m + 1] = fmax(mx[4 * m + 1], v);
-          mx[4 * m + 2] = fmax(mx[4 * m + 2], -r);
-          mx[4 * m + 3] = fmax(mx[4 * m + 3], r);
-        }
-        if (mm) { key[k] = okey(v); pk[k] = mm << FR_MSH; }
+      for (int m = 0; m < 2; ++m) {
+        if (!act[m]) continue;
+        const double r = rr[m][i];
+        if (r != r) continue;
+        mm |= 1 << m;
+        v1[2 * m] += v;
+        v1[2 * m + 1] += r;
+        mx[4 * m + 0] = fmax(mx[4 * m + 0], -v);
+        mx[4 * m + 1] = fmax(mx[4 * m + 1], v);
+        mx[4 * m + 2] = fmax(mx[4 * m + 2], -r);
+        mx[4 * m + 3] = fmax(mx[4 * m + 3], r);
       }
+      if (mm) { key[k] = okey(v); pk[k] = mm << FR_MSH; }
     }
+    cw0 += __popcll(__ballot(mm & 1));
+    cw1 += __popcll(__ballot(mm & 2));
   }
   const uint64_t smp = wid == 0 ? fr_sample(xf, nullptr, A) : KEY_SENTINEL;
   for (int b = t; b <= NB; b += NT) cnt[b] = 0;
-  fr_part_bfly<8, false>(v1, dscr, 16, 0);
+  fr_part_bfly<4, false>(v1, dscr, 16, 0);
+  if ((t & 63) == 0) {
+    dscr[wid * 16 + 4] = (double)cw0;
+    dscr[wid * 16 + 5] = (double)cw1;
+    dscr[wid * 16 + 6] = 0.0;
+    dscr[wid * 16 + 7] = 0.0;
+  }
   fr_part_bfly<8, true>(mx, dscr, 16, 8);
   fr_fin_dpp<NT>(dscr, 16, 8);
-  const double* tot1 = dscr + NW * 16;        // sums [0,6), -min/max [8,16)
+  const double* tot1 = dscr + NW * 16;        // f0, r0, f1, r1 sums, n0, n1 [0,6); -min/max [8,16)
+  double tot[6];                              // block-uniform: kept in SGPRs
 #pragma unroll
-  for (int q = 0; q < 6; ++q) v1[q] = tot1[q];
+  for (int q = 0; q < 6; ++q) tot[q] = fr_uniform_d(tot1[q]);
   BR_PH();
   __shared__ double cst[8];                   // only thread 0 reads them back
   if (t == 0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) cst[q] = tot1[8 + q];
   }
-  const int n[2] = {(int)v1[0], (int)v1[1]};
-  const bool need = (act[0] && n[0] >= 3) || (act[1] && n[1] >= 3);
+  // pair counts as (exact) doubles: they stay in SGPRs, an int copy would live in VGPRs
+  const double n[2] = {tot[4], tot[5]};
+  const bool need = (act[0] && n[0] >= 3.0) || (act[1] && n[1] >= 3.0);
   __shared__ double fin[16];                  // per-lag moment totals (thread 0)
   if (need) {
     if (wid == 0) {
@@ -532,67 +546,100 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
     __syncthreads();
     fr_scan<NT, u64>(cnt, NB, uscr);
     BR_PH();
-    // a0[k] / a1[k] = #less | #equal << 16 among the bucket's lag-0 / lag-1 members;
-    // sl[k] = bucket start | scan length << 16 (packed: the kernel runs at 64 VGPRs)
-    int sl[EMAX], a0[EMAX], a1[EMAX];
-    int maxlen = 0;
+    // Counters -> registers: a0[k] / a1[k] = the lag's rank base (members of lower
+    // buckets) | #equal << 16 for elements whose bucket needs no scan.  pk[k] becomes the
+    // element's slot in bucket order (every pair-valid element has a unique one) | lag
+    // mask << FR_MSH.  Elements of buckets to scan park the member count in a0's #equal
+    // half and the bucket start in a1 bits 14..27, flagged by a1's sign bit.
+    int a0[EMAX], a1[EMAX];
+    const int nmem = (int)(cnt[NB] & 0xffff);   // pair-valid elements (either lag)
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      sl[k] = 0; a0[k] = 0; a1[k] = 0;
+      a0[k] = 0; a1[k] = 0;
       if (key[k] == KEY_SENTINEL) continue;
       const int b = (pk[k] >> PK_BSHIFT) & FR_BMASK;
       const int mk = pk[k] >> FR_MSH;
       const u64 c0 = cnt[b], dc = cnt[b + 1] - c0;
       const int nall = (int)(dc & 0xffff);
       const int s0 = (int)(c0 & 0xffff);
-      int len = 0;
+      const int b0 = (int)((c0 >> 16) & 0xffff), b1 = (int)((c0 >> 32) & 0xffff);
       if ((b % (K + 1)) == K) {
-        a0[k] = (int)((dc >> 16) & 0xffff) << 16;
-        a1[k] = (int)((dc >> 32) & 0xffff) << 16;
+        a0[k] = b0 | ((int)((dc >> 16) & 0xffff) << 16);
+        a1[k] = b1 | ((int)((dc >> 32) & 0xffff) << 16);
       } else if (nall == 1) {
-        a0[k] = (mk & 1) << 16;
-        a1[k] = (mk >> 1) << 16;
+        a0[k] = b0 | ((mk & 1) << 16);
+        a1[k] = b1 | ((mk >> 1) << 16);
       } else {
-        len = nall;
-        const int q = s0 + (pk[k] & PK_SLOT);
-        bkey[q] = key[k];
-        bmask[q] = (uint8_t)mk;
+        a0[k] = b0 | (nall << 16);
+        a1[k] = b1 | (s0 << 14) | (int)0x80000000u;
       }
-      sl[k] = s0 | (len << 16);
-      maxlen = max(maxlen, len);
+      pk[k] = (s0 + (pk[k] & PK_SLOT)) | (mk << FR_MSH);
+    }
+    __syncthreads();                          // counters dead: bucket-ordered arrays reuse them
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      if (key[k] == KEY_SENTINEL) continue;
+      const int q = pk[k] & PK_SLOT;
+      const bool scan = a1[k] < 0;
+      bkey[q] = key[k];
+      binfo[q] = scan ? ((uint32_t)((a1[k] >> 14) & 0x3fff) | ((uint32_t)a0[k] & 0xffff0000u)) : 0u;
+      bmask[q] = (uint8_t)(pk[k] >> FR_MSH);
+      if (scan) { a0[k] &= 0xffff; a1[k] &= 0x3fff; }
     }
     __syncthreads();
     BR_PH();
-    for (int j = 0; j < maxlen; ++j) {
+    // In-bucket scan, position-parallel: thread t takes bucket-ordered slots t + i*NT, so a
+    // large bucket (tie cluster, dense tail) is spread over consecutive lanes of one or two
+    // waves instead of stretching every wave's loop.  res = #less | #equal << 16 per lag;
+    // lag 0's goes straight into the slot's own binfo word (read only by its owner), lag
+    // 1's over the key after a barrier.  Slots of buckets without a scan end with 0 in both.
+    uint32_t res1[EMAX];
 #pragma unroll
-      for (int k = 0; k < EMAX; ++k) {
-        if (j < (sl[k] >> 16)) {
-          const int q = (sl[k] & 0xffff) + j;
-          const uint64_t w = bkey[q];
-          const int wm = bmask[q];
-          const int inc = (w < key[k]) + ((w == key[k]) << 16);
-          a0[k] += (wm & 1) ? inc : 0;
-          a1[k] += (wm & 2) ? inc : 0;
-        }
+    for (int i = 0; i < EMAX; ++i) {
+      res1[i] = 0;
+      const int q = t + i * NT;
+      if (q >= nmem) continue;
+      const uint32_t in = binfo[q];
+      const int len = (int)(in >> 16);
+      if (len == 0) continue;
+      const int st = (int)(in & 0xffff);
+      const uint64_t me = bkey[q];
+      uint32_t r0 = 0;
+      for (int j = 0; j < len; ++j) {
+        const uint64_t w = bkey[st + j];
+        const uint32_t wm = bmask[st + j];
+        const uint32_t inc = (w < me ? 1u : 0u) + (w == me ? 0x10000u : 0u);
+        r0 += (wm & 1) ? inc : 0u;
+        res1[i] += (wm & 2) ? inc : 0u;
       }
+      binfo[q] = r0;
     }
+    __syncthreads();                          // all scans done: lag-1 results overwrite the keys
+    uint32_t* bres1 = reinterpret_cast<uint32_t*>(bkey);
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      const int q = t + i * NT;
+      if (q < nmem) bres1[2 * q] = res1[i];
+    }
+    __syncthreads();
+    BR_PH();
     // pk[k] <- 2*rank(lag 0) | 2*rank(lag 1) << 16 (half-integer ranks, exact); a field is
     // 0 when the element is not a member of that lag's pairs
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       if (key[k] == KEY_SENTINEL) continue;
       const int mk = pk[k] >> FR_MSH;
-      const u64 c0 = cnt[(pk[k] >> PK_BSHIFT) & FR_BMASK];
-      const int b0 = (int)((c0 >> 16) & 0xffff), b1 = (int)((c0 >> 32) & 0xffff);
-      pk[k] = ((mk & 1) ? (2 * (b0 + (a0[k] & 0xffff)) + (a0[k] >> 16) + 1) : 0) |
-              ((mk & 2) ? ((2 * (b1 + (a1[k] & 0xffff)) + (a1[k] >> 16) + 1) << 16) : 0);
+      a0[k] += (int)binfo[pk[k] & PK_SLOT];
+      a1[k] += (int)bres1[2 * (pk[k] & PK_SLOT)];
+      pk[k] = ((mk & 1) ? (2 * (a0[k] & 0xffff) + (a0[k] >> 16) + 1) : 0) |
+              ((mk & 2) ? ((2 * (a1[k] & 0xffff) + (a1[k] >> 16) + 1) << 16) : 0);
     }
     double fm[2], rm[2], km[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      const double dn = (double)n[m];
-      fm[m] = v1[2 + 2 * m] / dn;
-      rm[m] = v1[3 + 2 * m] / dn;
+      const double dn = n[m];
+      fm[m] = tot[2 * m] / dn;
+      rm[m] = tot[2 * m + 1] / dn;
       km[m] = (dn + 1.0) / 2.0;
     }
     BR_PH();
@@ -626,9 +673,9 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
       const int64_t td = s + lagv[m];
       double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
       const int64_t stp = F * D;
-      const int nn = n[m];
+      const double nn = n[m];
       double ic = qnan(), ric = qnan(), beta = qnan();
-      if (nn >= 3) {
+      if (nn >= 3.0) {
         const double* w = fin + 8 * m;
         const bool fconst = (-cst[4 * m + 0]) == cst[4 * m + 1];
         const bool rconst = (-cst[4 * m + 2]) == cst[4 * m + 3];
@@ -638,7 +685,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
         }
         beta = w[5] > 0 ? w[6] / w[5] : qnan();
       }
-      o[0] = (double)nn;
+      o[0] = nn;
       o[stp] = ic;
       o[2 * stp] = ric;
       o[3 * stp] = beta;

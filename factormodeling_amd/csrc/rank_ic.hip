@@ -24,7 +24,8 @@ __global__ void k_ic_empty(double* out, int64_t F, int64_t D, int L0, int L1, in
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                        const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
   const int nt = br_nt(1024);
-  const size_t lds_fr = (size_t)A * 8 + (size_t)((A + 15) & ~15ll);
+  // counters, then keys [A] + member info [A] + lag masks [A] (k_ic_daily_fr)
+  const size_t lds_fr = std::max<size_t>((size_t)(FRG<FR_K_IC>::NB + 1) * 8, (size_t)A * 13 + 16);
   auto fr_table = FMX_EMAX_TABLE(k_ic_daily_fr);
   const bool fine = rank_impl() == RANK_IMPL_FINE && lds_fits(fr_table(nt, br_emax(A, nt)), lds_fr);
   const size_t lds = fine ? lds_fr : (size_t)std::max<int64_t>(A, nt) * 8 + (size_t)((A + 15) & ~15ll);

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include "../../include/fmx.h"
 #include "fmx_common.hpp"
+#include "rowkit.hpp"
 
 namespace fmx {
 
@@ -201,9 +202,362 @@ __global__ void k_mm_combine(const double* __restrict__ Wf, const double* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Daily trade list, method 'linear' (portfolio_simulation.py:172-181): weights = the
+// signal on its positive / negative cells, _normalize_legs (:250-262) and
+// _cap_and_redistribute (:264-313) with max_iter 10, tol 1e-6.  One workgroup per date;
+// thread t holds the row cells t + k*LIN_NT in registers.  Every pandas sum the reference
+// takes -- w_pos.sum() over the date's n rows (zeros included), capped[capped > 0].sum(),
+// uncapped_long.sum(), ... -- is numpy's pairwise sum over that subset in symbol order, so
+// each subset is compacted into LDS (ballot prefix per register chunk) and summed with
+// the numpy schedule for its length (rowkit.hpp): the weights are bit-identical.  pandas
+// clip is where(x >= lo, x, lo) then where(x <= hi, x, hi).
+constexpr int LIN_NT = 1024;
+constexpr int LIN_NW = LIN_NT / 64;
+
+// Compact the cells whose bit k of `flags` is set, in asset order, into sub[0..m); all
+// threads get m.  wtot: EMAX * LIN_NW ints of scratch.
+template <int EMAX>
+__device__ int lin_compact(const double* v, uint32_t flags, double* sub, int* wtot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int pre[EMAX];
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const uint64_t b = __ballot((flags >> k) & 1u);
+    pre[k] = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[k * LIN_NW + wid] = __popcll(b);
+  }
+  __syncthreads();
+  if (wid == 0) {                       // exclusive scan over (chunk, wave) in asset order
+    constexpr int N = EMAX * LIN_NW, PER = (N + 63) / 64;
+    int loc[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { const int i = lane * PER + j; loc[j] = i < N ? wtot[i] : 0; sum += loc[j]; }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(incl, o, 64); if (lane >= o) incl += u; }
+    int run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { const int i = lane * PER + j; if (i < N) wtot[i] = run; run += loc[j]; }
+    if (lane == 63) wtot[N] = incl;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k)
+    if ((flags >> k) & 1u) sub[wtot[k * LIN_NW + wid] + pre[k]] = v[k];
+  const int m = wtot[EMAX * LIN_NW];
+  __syncthreads();
+  return m;
+}
+
+template <int EMAX>
+__device__ double lin_sum(const double* v, uint32_t flags, double* sub, int* wtot, PwTable pw, double* nodes,
+                          int* iscr) {
+  const int m = lin_compact<EMAX>(v, flags, sub, wtot);
+  int cnt;
+  return block_pw_sum_w0<LIN_NT>([&](int i) { return sub[i]; }, [](int) { return 0; }, pw.get(m), nodes, iscr,
+                                 &cnt);
+}
+
+template <int EMAX>
+__global__ void __launch_bounds__(LIN_NT)
+k_trade_linear(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
+               double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double mw,
+               PwTable pw) {
+  extern __shared__ double sub[];                 // [A] compacted subset
+  __shared__ double nodes[2 * (16384 / 64) + 8];
+  __shared__ int iscr[LIN_NW + 2];
+  __shared__ int wtot[EMAX * LIN_NW + 1];
+  const int t = threadIdx.x;
+  const int64_t d = blockIdx.x;
+  const double* x = X + d * A;
+  const uint8_t* p = present ? present + d * A : nullptr;
+  double w[EMAX];
+  uint32_t pm = 0, fpos = 0, fneg = 0;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int64_t a = t + (int64_t)k * LIN_NT;
+    const bool pr = a < A && (!p || p[a]);
+    const double v = pr ? x[a] : 0.0;
+    pm |= (uint32_t)pr << k;
+    fpos |= (uint32_t)(pr && v > 0.0) << k;
+    fneg |= (uint32_t)(pr && v < 0.0) << k;
+    w[k] = (pr && (v > 0.0 || v < 0.0)) ? v : 0.0;  // weights[pos.index] = pos, [neg.index] = neg
+  }
+  int c3[3] = {(int)__popc(pm), (int)__popc(fpos), (int)__popc(fneg)};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c3[i] += __shfl_xor(c3[i], o);
+  }
+  if ((t & 63) == 0) { iscr[t >> 6] = c3[1]; wtot[t >> 6] = c3[2]; }
+  __syncthreads();
+  int npos = 0, nneg = 0;
+  for (int i = 0; i < LIN_NW; ++i) { npos += iscr[i]; nneg += wtot[i]; }
+  const bool anyrow = __syncthreads_or(pm != 0);
+  const bool flat = npos == 0 || nneg == 0;
+  if (!flat) {
+    // _normalize_legs: w_pos = clip(lower=0), w_neg = clip(upper=0), sums over all n rows
+    double wp[EMAX], wn[EMAX];
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) { wp[k] = w[k] >= 0.0 ? w[k] : 0.0; wn[k] = w[k] <= 0.0 ? w[k] : 0.0; }
+    const double sp = lin_sum<EMAX>(wp, pm, sub, wtot, pw, nodes, iscr);
+    const double sn = lin_sum<EMAX>(wn, pm, sub, wtot, pw, nodes, iscr);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const double a = sp > 0.0 ? wp[k] / sp : wp[k];
+      const double b = sn < 0.0 ? wn[k] / -sn : wn[k];
+      w[k] = a + b;
+    }
+    // _cap_and_redistribute(max_weight, max_iter=10, tol=1e-6)
+    const double tol = 1e-6;
+    for (int it = 0; it < 10; ++it) {
+      double c[EMAX];
+      uint32_t fcp = 0, fcn = 0, ful = 0, fus = 0;
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        double v = w[k] >= -mw ? w[k] : -mw;
+        v = v <= mw ? v : mw;
+        c[k] = v;
+        const uint32_t pr = (pm >> k) & 1u;
+        fcp |= (pr & (uint32_t)(v > 0.0)) << k;
+        fcn |= (pr & (uint32_t)(v < 0.0)) << k;
+        ful |= (pr & (uint32_t)(w[k] > 0.0 && v < mw)) << k;
+        fus |= (pr & (uint32_t)(w[k] < 0.0 && v > -mw)) << k;
+      }
+      const double le = 1.0 - lin_sum<EMAX>(c, fcp, sub, wtot, pw, nodes, iscr);
+      const double se = -1.0 - lin_sum<EMAX>(c, fcn, sub, wtot, pw, nodes, iscr);
+      const bool any_ul = __syncthreads_or(ful != 0), any_us = __syncthreads_or(fus != 0);
+      if ((fabs(le) < tol && fabs(se) < tol) || (!any_ul && !any_us)) break;
+      if (any_ul && fabs(le) > tol) {
+        const double su = lin_sum<EMAX>(c, ful, sub, wtot, pw, nodes, iscr);
+#pragma unroll
+        for (int k = 0; k < EMAX; ++k)
+          if ((ful >> k) & 1u) c[k] = c[k] + le * (c[k] / su);
+      }
+      if (any_us && fabs(se) > tol) {
+        const double su = lin_sum<EMAX>(c, fus, sub, wtot, pw, nodes, iscr);
+#pragma unroll
+        for (int k = 0; k < EMAX; ++k)
+          if ((fus >> k) & 1u) c[k] = c[k] + se * (c[k] / su);
+      }
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) w[k] = c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      double v = w[k] >= -mw ? w[k] : -mw;
+      w[k] = v <= mw ? v : mw;
+    }
+  }
+  double* wr = W + d * A;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int64_t a = t + (int64_t)k * LIN_NT;
+    if (a >= A) continue;
+    const double out = ((pm >> k) & 1u) ? (flat ? 0.0 : w[k]) : __builtin_nan("");
+    wr[a] = out;
+    if (Wshift) {
+      if (d + 1 < D) Wshift[(d + 1) * A + a] = out;
+      if (d == 0) Wshift[a] = __builtin_nan("");
+    }
+  }
+  if (t == 0) {                                   // counts (len(pos), len(neg)); NaN: no rows
+    counts[2 * d] = anyrow ? (flat ? 0.0 : (double)npos) : __builtin_nan("");
+    counts[2 * d + 1] = anyrow ? (flat ? 0.0 : (double)nneg) : __builtin_nan("");
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Simulation._daily_portfolio_returns (portfolio_simulation.py:748-797)
+// on the aligned [D][A] grid (union of the weights' and returns' dates and symbols; NaN =
+// a cell the reference's unstack().fillna(0) makes 0).  One workgroup per date row:
+//   longs = max(w, 0), shorts = |min(w, 0)|
+//   out[d][0] = sum longs * r            (long_ret_raw, :758)
+//   out[d][1] = sum shorts * r           (short_ret_raw = -out[1], :759)
+//   out[d][2] = sum |longs - longs_prev|  (long turnover, :761; prev = previous weights date)
+//   out[d][3] = sum |shorts - shorts_prev|
+//   out[d][4] = sum |d longs| * rate(cap) (long cost, :766-767; rate 1 -> 0.0025, 2 -> 0.0015,
+//   out[d][5] = sum |d shorts| * rate(cap)   3 -> 0.0010, other ints as themselves, :764-765)
+// wprev[d] = row of the previous weights date (-1: first weights date or not one: no diff).
+// Block sums are deterministic (fixed lane/wave order); the reference sums rows with
+// numpy (order differs in the last bits only).
+constexpr int PNL_NT = 256;
+__device__ __forceinline__ double cap_rate(double c) {
+  const double ci = (c == c) ? trunc(c) : 0.0;   // fillna(0).astype(int)
+  return ci == 1.0 ? 0.0025 : ci == 2.0 ? 0.0015 : ci == 3.0 ? 0.0010 : ci;
+}
+__device__ __forceinline__ double nz(double v) { return v == v ? v : 0.0; }
+
+template <int N>
+__device__ __forceinline__ void pnl_block_sum(double* v, double* scr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o);
+    if (lane == 0) scr[wid * N + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double t = 0.0;
+    for (int w = 0; w < PNL_NT / 64; ++w) t += scr[w * N + i];
+    v[i] = t;
+  }
+}
+
+__global__ void __launch_bounds__(PNL_NT)
+k_pnl_daily(const double* __restrict__ W, const double* __restrict__ R, const double* __restrict__ CAP,
+            const int32_t* __restrict__ wprev, double* __restrict__ out, int64_t A) {
+  __shared__ double scr[(PNL_NT / 64) * 6];
+  const int64_t d = blockIdx.x;
+  const int64_t pv = wprev[d];
+  const double* w = W + d * A;
+  const double* r = R + d * A;
+  const double* wp = pv >= 0 ? W + pv * A : nullptr;
+  const double* cp = CAP ? CAP + d * A : nullptr;
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t a = threadIdx.x; a < A; a += PNL_NT) {
+    const double wv = nz(w[a]), rv = nz(r[a]);
+    const double l = wv > 0.0 ? wv : 0.0, sh = wv < 0.0 ? -wv : 0.0;
+    acc[0] += l * rv;
+    acc[1] += sh * rv;
+    if (wp) {
+      const double pw = nz(wp[a]);
+      const double pl = pw > 0.0 ? pw : 0.0, ps = pw < 0.0 ? -pw : 0.0;
+      const double dl = fabs(l - pl), ds = fabs(sh - ps);
+      const double rate = cp ? cap_rate(cp[a]) : 0.0;
+      acc[2] += dl;
+      acc[3] += ds;
+      acc[4] += dl * rate;
+      acc[5] += ds * rate;
+    }
+  }
+  pnl_block_sum<6>(acc, scr);
+  if (threadIdx.x < 6) out[d * 6 + threadIdx.x] = acc[threadIdx.x];
+}
+
+// Per-symbol contributions (contributor=True, :790-793): column sums over the dates of
+// longs * r - |d longs| * rate (and the short leg with -shorts * r).  One lane per asset.
+__global__ void k_pnl_contrib(const double* __restrict__ W, const double* __restrict__ R,
+                              const double* __restrict__ CAP, const int32_t* __restrict__ wprev,
+                              double* __restrict__ out, int64_t D, int64_t A) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A) return;
+  double lp = 0.0, sp = 0.0, lc = 0.0, sc = 0.0;
+  for (int64_t d = 0; d < D; ++d) {
+    const double wv = nz(W[d * A + a]), rv = nz(R[d * A + a]);
+    const double l = wv > 0.0 ? wv : 0.0, sh = wv < 0.0 ? -wv : 0.0;
+    lp += l * rv;
+    sp += sh * rv;
+    const int64_t pv = wprev[d];
+    if (pv >= 0) {
+      const double pw = nz(W[pv * A + a]);
+      const double pl = pw > 0.0 ? pw : 0.0, ps = pw < 0.0 ? -pw : 0.0;
+      const double rate = CAP ? cap_rate(CAP[d * A + a]) : 0.0;
+      lc += fabs(l - pl) * rate;
+      sc += fabs(sh - ps) * rate;
+    }
+  }
+  out[2 * a] = lp - lc;
+  out[2 * a + 1] = -sp - sc;
+}
+
+// _calculate_metrics daily IC (portfolio_simulation.py:799-805): per date, pandas
+// Series.corr = np.corrcoef of the pair-valid (alpha, ret) cells: two passes (means, then
+// centred cross / square sums), r = (c01 / sd0) / sd1 clipped to [-1, 1]; NaN for n < 2
+// or a constant side.  out[d] = (n, corr).
+__global__ void __launch_bounds__(PNL_NT)
+k_daily_corr(const double* __restrict__ X, const double* __restrict__ R, double* __restrict__ out, int64_t A) {
+  __shared__ double scr[(PNL_NT / 64) * 3];
+  const int64_t d = blockIdx.x;
+  const double* x = X + d * A;
+  const double* r = R + d * A;
+  double s[3] = {0, 0, 0};                      // n, sum x, sum r
+  for (int64_t a = threadIdx.x; a < A; a += PNL_NT) {
+    const double xv = x[a], rv = r[a];
+    if (xv == xv && rv == rv) { s[0] += 1.0; s[1] += xv; s[2] += rv; }
+  }
+  pnl_block_sum<3>(s, scr);
+  const double n = s[0], mx = s[1] / n, mr = s[2] / n;
+  __syncthreads();
+  double c[3] = {0, 0, 0};                      // sum dx dr, dx^2, dr^2
+  for (int64_t a = threadIdx.x; a < A; a += PNL_NT) {
+    const double xv = x[a], rv = r[a];
+    if (xv == xv && rv == rv) {
+      const double dx = xv - mx, dr = rv - mr;
+      c[0] += dx * dr; c[1] += dx * dx; c[2] += dr * dr;
+    }
+  }
+  pnl_block_sum<3>(c, scr);
+  if (threadIdx.x == 0) {
+    double v = __builtin_nan("");
+    if (n >= 2.0) {
+      const double f = n - 1.0;
+      const double c01 = c[0] / f, sd0 = sqrt(c[1] / f), sd1 = sqrt(c[2] / f);
+      v = (c01 / sd0) / sd1;
+      if (v == v) v = fmin(1.0, fmax(-1.0, v));
+    }
+    out[2 * d] = n;
+    out[2 * d + 1] = v;
+  }
+}
+
 }  // namespace fmx
 
 using namespace fmx;
+
+extern "C" fmx_status fmx_trade_linear(const double* X, const uint8_t* present, double* Wraw, double* Wout,
+                                       double* counts, int64_t D, int64_t A, double max_weight, void* stream) {
+  FMX_ARG(X && Wraw && Wout && counts && D >= 0 && A >= 0, "bad args");
+  FMX_ARG(Wraw != Wout && Wraw != X, "Wraw must not alias X or Wout");
+  FMX_ARG(A <= 16384, "trade list holds one date row per workgroup: A <= 16384");
+  if (D == 0 || A == 0) return FMX_OK;
+  FMX_ARG(D <= 0x7fffffffll, "too many dates");
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  const int E = (int)ceil_div(A, LIN_NT);
+  const void* k = E <= 1 ? (const void*)k_trade_linear<1> : E <= 2 ? (const void*)k_trade_linear<2>
+                : E <= 4 ? (const void*)k_trade_linear<4> : E <= 8 ? (const void*)k_trade_linear<8>
+                           : (const void*)k_trade_linear<16>;
+  const size_t lds = (size_t)A * sizeof(double);
+  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  double* ws = present ? nullptr : Wout;
+  void* args[] = {(void*)&X, (void*)&present, (void*)&Wraw, (void*)&ws, (void*)&counts, (void*)&D, (void*)&A,
+                  (void*)&max_weight, (void*)&pw};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D), dim3(LIN_NT), args, lds, as_stream(stream)));
+  if (!present) return FMX_OK;
+  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG));
+  k_shift_rows<<<g, 256, 0, as_stream(stream)>>>(Wraw, Wout, D, A);
+  FMX_LAUNCH_CHECK("k_shift_rows");
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_pnl_daily(const double* W, const double* R, const double* CAP, const int32_t* wprev,
+                                    double* out, double* contrib, int64_t D, int64_t A, void* stream) {
+  FMX_ARG(W && R && wprev && out && D >= 0 && A >= 0, "bad args");
+  if (D == 0) return FMX_OK;
+  FMX_ARG(D <= 0x7fffffffll, "too many dates");
+  k_pnl_daily<<<(unsigned)D, PNL_NT, 0, as_stream(stream)>>>(W, R, CAP, wprev, out, A);
+  FMX_LAUNCH_CHECK("k_pnl_daily");
+  if (contrib && A > 0) {
+    k_pnl_contrib<<<(unsigned)ceil_div(A, 256), 256, 0, as_stream(stream)>>>(W, R, CAP, wprev, contrib, D, A);
+    FMX_LAUNCH_CHECK("k_pnl_contrib");
+  }
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_daily_corr(const double* X, const double* R, double* out, int64_t D, int64_t A,
+                                     void* stream) {
+  FMX_ARG(X && R && out && D >= 0 && A >= 0, "bad args");
+  if (D == 0) return FMX_OK;
+  FMX_ARG(D <= 0x7fffffffll, "too many dates");
+  k_daily_corr<<<(unsigned)D, PNL_NT, 0, as_stream(stream)>>>(X, R, out, A);
+  FMX_LAUNCH_CHECK("k_daily_corr");
+  return FMX_OK;
+}
 
 extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
                                       double* counts, int64_t D, int64_t A, double pct, void* stream) {

@@ -459,3 +459,40 @@ def mm_combine(Wf, counts, fw, colmap, wdate):
     call("fmx_mm_combine", ptr(Wf.contiguous()), ptr(counts.contiguous()), ptr(fw_d), ptr(cm_d), ptr(wd_d),
          ptr(out), ptr(oc), Fw, Dw, D, A, stream_ptr())
     return out, oc
+
+
+# ----------------------------------------------------------------------------- P&L
+def _dense2(X, name):
+    if X.dim() != 2 or X.dtype != F64 or not X.is_cuda or not X.is_contiguous():
+        raise _lib.FmxError(f"{name} must be a contiguous float64 [D][A] device tensor")
+
+
+def pnl_daily(W, R, CAP, wprev, contrib=False):
+    """Simulation._daily_portfolio_returns per-date sums (fmx_pnl_daily): [D][6] and the
+    optional per-symbol [A][2] contributions."""
+    _dense2(W, "W")
+    _dense2(R, "R")
+    D, A = W.shape
+    if tuple(R.shape) != (D, A) or (CAP is not None and (tuple(CAP.shape) != (D, A))):
+        raise _lib.FmxError("pnl_daily: shape mismatch")
+    if CAP is not None:
+        _dense2(CAP, "CAP")
+    wp = torch.as_tensor(np.ascontiguousarray(np.asarray(wprev, dtype=np.int32)), device=W.device)
+    if wp.numel() != D or (wp >= D).any():
+        raise _lib.FmxError("pnl_daily: wprev must be [D] row indices < D (or -1)")
+    out = torch.empty((D, 6), dtype=F64, device=W.device)
+    cb = torch.empty((A, 2), dtype=F64, device=W.device) if contrib else None
+    call("fmx_pnl_daily", ptr(W), ptr(R), ptr(CAP), ptr(wp), ptr(out), ptr(cb), D, A, stream_ptr())
+    return out, cb
+
+
+def daily_corr(X, R):
+    """Per-date Pearson (np.corrcoef) of pair-valid cells (fmx_daily_corr): [D][2] = (n, corr)."""
+    _dense2(X, "X")
+    _dense2(R, "R")
+    D, A = X.shape
+    if tuple(R.shape) != (D, A):
+        raise _lib.FmxError("daily_corr: shape mismatch")
+    out = torch.empty((D, 2), dtype=F64, device=X.device)
+    call("fmx_daily_corr", ptr(X), ptr(R), ptr(out), D, A, stream_ptr())
+    return out

@@ -239,6 +239,19 @@ fmx_status fmx_mm_combine(const double* Wf, const double* counts, const double* 
                           const int32_t* wdate, double* out, double* out_counts, int64_t Fw, int64_t Dw,
                           int64_t D, int64_t A, void* stream);
 
+/* ---- portfolio P&L (portfolio_simulation.py:748-819) ---------- */
+/* Replaces Simulation._daily_portfolio_returns' per-date sums on the aligned [D][A] grid
+ * (union of the weights' and returns' dates/symbols; NaN cells count as 0 as after
+ * unstack().fillna(0)): W shifted weights, R returns, CAP cap flags (or NULL: no cost),
+ * wprev [D] = row of the previous weights date (-1: none).  out [D][6] = (sum longs*r,
+ * sum shorts*r, long turnover, short turnover, long cost, short cost); contrib [A][2]
+ * (optional) = per-symbol long / short P&L net of cost (contributor=True, :790-793). */
+fmx_status fmx_pnl_daily(const double* W, const double* R, const double* CAP, const int32_t* wprev, double* out,
+                         double* contrib, int64_t D, int64_t A, void* stream);
+/* Replaces _calculate_metrics' daily IC (:799-805): per date, Series.corr (np.corrcoef) of
+ * the pair-valid (X, R) cells.  out [D][2] = (n, corr); corr NaN for n < 2 or constant. */
+fmx_status fmx_daily_corr(const double* X, const double* R, double* out, int64_t D, int64_t A, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
