@@ -1,6 +1,6 @@
 """Benchmark: factor·asset·days/s of the device-resident ops + IC + selection pipeline.
 
-    python bench.py --gpus N --steps K --warmup W [--dates D --assets A --factors F]
+    python bench.py --gpus N --steps K --warmup W [--workload c2|c4|c5] [--dates D ...]
 
 Default workload = BASELINE.json configs[1] (C2): 2,520 dates x 5,000 assets x 200
 factors, synthetic data (SURVEY 8(d) generator, generated on the device).  A "step" is
@@ -10,9 +10,16 @@ every processed day, fp64-MFMA factor Gram + greedy pruning).  For N > 1 the pan
 sharded by date (strong scaling: the same panel over N GPUs) with a halo exchange,
 an IC all-gather and a Gram all-reduce over RCCL.
 
+Other workloads (BASELINE configs[3], [4]; parity cases, not the driver's line):
+  c4  2,520 x 3,000 x 2,000 factor zoo: daily IC + full-sample metrics for the pruning
+      order, the 2,000 x 2,000 correlation Gram (fp64 MFMA, chunked by date) + greedy prune;
+  c5  2,520 x 10,000 x 500: ts_corr(x, R, 60) and ts_std(60) over factor chunks, daily IC
+      lags 1-2, 60-day window metrics, icir_top weights, weighted composite (zscore).
+
 Rank 0 prints one JSON line (driver contract) with ``roofline`` (dominant kernel,
-HIP-event timed inside the timed steps) and ``cpu_baseline`` (the numpy oracle port on
-a bounded sample, 1 host core).
+HIP-event timed inside the timed steps), ``cpu_baseline`` (the numpy oracle port on a
+bounded sample, 16 host processes) and ``reference_cpu`` (the reference itself, timed in
+the build container: SURVEY.md §6).
 """
 from __future__ import annotations
 
@@ -42,6 +49,8 @@ def bytes_per_unit(stage, F):
         return 48.0
     if kind in ("cs_zscore_neutralize", "cs_rank_winsor"):   # X once + two outputs
         return 24.0
+    if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
+        return 16.0
     if kind == "ic_daily":
         return 8.0 + 16.0 / F
     return None
@@ -76,48 +85,111 @@ def pmc_traffic(stage, dims):
     return None
 
 
+# BASELINE.json configs: [1] C2, [3] C4, [4] C5 (D unspecified there: 2520)
+WORKLOAD_DIMS = {"c2": (2520, 5000, 200), "c4": (2520, 3000, 2000), "c5": (2520, 10000, 500)}
+WORKLOAD_NAME = {"c2": "C2 ops+IC+icir_top+corr-prune",
+                 "c4": "C4 wide zoo: IC order + 2000x2000 corr Gram (fp64 MFMA) + greedy prune",
+                 "c5": "C5 ts_corr/ts_std(60) + rolling-IC icir_top + weighted composite"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--dates", type=int, default=2520)
-    p.add_argument("--assets", type=int, default=5000)
-    p.add_argument("--factors", type=int, default=200)
+    p.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    p.add_argument("--dates", type=int, default=None)
+    p.add_argument("--assets", type=int, default=None)
+    p.add_argument("--factors", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample-factors", type=int, default=1)
+    p.add_argument("--cpu-workers", type=int, default=16, help="host processes of the CPU port baseline")
     p.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     p.add_argument("--selftest-dist", action="store_true",
                    help="CPU/gloo check of the rank launcher only (tests/test_bench_launch.py)")
     return p.parse_args()
 
 
-def cpu_baseline(D, A, seed=0):
-    """Time the numpy oracle port (test infrastructure; 1 core) on a bounded sample of the
-    same workload: one factor over a 2520 x A slice for the operator set, plus daily IC
-    over 120 dates.  Returns (factor·asset·days/s, description)."""
+def _port_worker(args):
+    """One factor of the C2 step on the numpy oracle port (test infrastructure; a child
+    process, no GPU): the 9 operators over all dates, daily IC lags 1-2 on a date sample
+    (scaled), and the factor's exposures for the Gram.  Returns timings."""
+    D, A, seed, ic_dates = args
+    sys.path.insert(0, ROOT)
     import oracle.metrics as OM
     import oracle.ops as O
     rng = np.random.default_rng(seed)
-    Ds = D
-    x = rng.standard_normal((Ds, A))
+    x = rng.standard_normal((D, A))
+    x = np.where(rng.random((D, A)) < 0.05, np.round(x, 1), x)
     x[rng.random(x.shape) < 0.01] = np.nan
-    r = 0.01 * rng.standard_normal((Ds, A))
+    r = 0.01 * rng.standard_normal((D, A))
     t0 = time.perf_counter()
     O.ts_mean(x, 20); O.ts_std(x, 20); O.ts_zscore(x, 20); O.ts_rank(x, 10); O.ts_decay(x, 20)
     O.cs_rank(x); O.cs_zscore(x); O.cs_winsor(x); O.market_neutralize(x)
     t_ops = time.perf_counter() - t0
-    Di = min(Ds, 252)
+    Di = min(D, ic_dates)
     t0 = time.perf_counter()
     for t in range(2, Di):
         OM.daily_stats(x[t - 1], r[t])
         OM.daily_stats(x[t - 2], r[t])
-    t_ic = (time.perf_counter() - t0) * (Ds / Di)
-    units = Ds * A
-    rate = units / (t_ops + t_ic)
-    return rate, (f"numpy oracle (single thread), 1 factor x {Ds} dates x {A} assets: 9 operators "
-                  f"({t_ops:.1f}s measured) + daily IC lags 1-2 ({t_ic:.1f}s, measured on {Di} dates, "
-                  f"scaled to {Ds}); window metrics/selection/Gram not included")
+    t_ic = (time.perf_counter() - t0) * (D / Di)
+    return t_ops, t_ic
+
+
+def cpu_baseline(D, A, workers=16, ic_dates=126):
+    """The numpy oracle PORT of the C2 step on ``workers`` host processes (one factor each,
+    all concurrent): operators + daily IC (sampled dates, scaled) per factor, then the
+    window metrics + icir_top selection over all processed days and the factor Gram of the
+    sampled factors.  Must run before this process touches the GPU (children are spawned).
+    Returns (factor·asset·days/s, cores, description)."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import oracle.gram as OG
+    import oracle.metrics as OM
+    Fs = workers
+    t0 = time.perf_counter()
+    with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+        res = list(ex.map(_port_worker, [(D, A, 1000 + f, ic_dates) for f in range(Fs)]))
+    t_spawned = time.perf_counter() - t0
+    # per-worker wall = ops + scaled IC; the concurrent run lasts as long as the slowest
+    t_par = max(a + b for a, b in res)
+    # window metrics (W = 60) + icir_top for every processed day over the sampled factors
+    rng = np.random.default_rng(7)
+    daily = rng.standard_normal((4, Fs, D)) * 0.05
+    daily[0] = A
+    t0 = time.perf_counter()
+    W = 60
+    for i in range(W, D - 1):
+        vals = np.array([OM.summarize(daily[1, f, i - W + 1:i], daily[2, f, i - W + 1:i], daily[3, f, i - W + 1:i])
+                         for f in range(Fs)])
+        OM.icir_top(OM.nargsort_desc(vals[:, 3]), vals, -1.0, 5)
+    t_sel = time.perf_counter() - t0
+    # Gram of the sampled factors over a date sample (scaled)
+    Dg = 63
+    Xg = rng.standard_normal((Fs, Dg, A))
+    t0 = time.perf_counter()
+    OG.corr_matrix(Xg)
+    t_gram = (time.perf_counter() - t0) * (D / Dg)
+    wall = t_par + t_sel + t_gram
+    units = float(Fs) * D * A
+    desc = (f"numpy oracle port on {workers} host processes (one factor each, concurrent): {Fs} factors x {D} dates "
+            f"x {A} assets; 9 operators + daily IC lags 1-2 ({ic_dates} dates measured, scaled) per factor "
+            f"(slowest worker {t_par:.1f}s), window metrics + icir_top for {D - W - 1} days ({t_sel:.1f}s), "
+            f"factor Gram ({Dg} dates measured, scaled: {t_gram:.1f}s); measured wall incl. process start "
+            f"{t_spawned:.1f}s")
+    return units / wall, workers, desc
+
+
+# SURVEY.md §6: the reference itself (pandas/scipy as-is, 1 core) timed in the build
+# container -- it cannot run on the GPU box (the reference never travels there).
+REFERENCE_CPU = {
+    "c1_measured": 3.25e4,
+    "c2_extrapolated": 1.1e4,
+    "unit": "factor·asset·days/s",
+    "cores": 1,
+    "source": "SURVEY.md §6: C1 (500x1000x20 ops+IC+select+composite) measured 307.4 s in the build container; "
+              "C2 extrapolated from measured C2 slices: 8 operators ~3,200 s + winsor ~3,500 s + ts_decay ~6,100 s "
+              "+ ts_rank ~159,000 s + single_factor_metrics ~1,700 s + FactorSelector ~57,500 s = ~2.3e5 s",
+}
 
 
 def spawn_ranks(n):
@@ -162,6 +234,12 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
+        # before this process initialises the GPU: the port's workers are spawned children
+        dims0 = WORKLOAD_DIMS[args.workload]
+        rate, cores, sample = cpu_baseline(args.dates or dims0[0], args.assets or dims0[1], args.cpu_workers)
+        cpu = {"value": rate, "unit": "factor·asset·days/s", "cores": cores, "kind": "port", "sample": sample}
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -169,9 +247,12 @@ def main():
     dev = torch.device("cuda", local)
     from factormodeling_amd import pipeline as PL
 
-    D, A, F = args.dates, args.assets, args.factors
-    sp = PL.ShardedPanel(D, A, F, rank, world, dev, seed=0)
-    cfg = PL.StepConfig()
+    dims = WORKLOAD_DIMS[args.workload]
+    D = args.dates or dims[0]
+    A = args.assets or dims[1]
+    F = args.factors or dims[2]
+    cfg = PL.workload_config(args.workload)
+    sp = PL.ShardedPanel(D, A, F, rank, world, dev, seed=0, halo=cfg.halo)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -204,16 +285,23 @@ def main():
     local_units = float(F) * (sp.X.shape[1]) * A
     achieved = bytes_per_unit(dom, F) * local_units / (dom_ms * 1e-3) / 1e9
     # whole-step algorithmic bytes per unit of the HBM-priced stages (+ the Gram's X read)
-    step_bpu = sum(bytes_per_unit(k, F) for k in op_stages) + 8.0
+    step_bpu = sum(bytes_per_unit(k, F) for k in op_stages) + (8.0 if cfg.gram else 0.0)
     traffic = pmc_traffic(dom, [sp.X.shape[1], A, F]) if world == 1 else None
+    roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "algorithmic_bytes": bytes_per_unit(dom, F) * local_units, "ms": dom_ms}
+    gram_ms = stages.get("gram", 0.0) / args.steps
+    if cfg.gram and gram_ms > dom_ms:
+        # the Gram dominates (C4): priced on MFMA -- the upper triangle incl. the diagonal of
+        # G = Z^T Z, D*A*F*(F+1) flop (SURVEY 8(d) quotes the full square, 2*D*A*F^2)
+        flops = float(sp.X.shape[1] - sp.halo) * A * F * (F + 1)
+        tf = flops / (gram_ms * 1e-3) / 1e12
+        roofline = {"kernel": "gram", "bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": tf / FP64_PEAK_TFS, "traffic": None, "algorithmic_flops": flops, "ms": gram_ms}
     if args.stages and rank == 0:
         for k, v in sorted(stages.items(), key=lambda kv: -kv[1]):
             print(f"stage {k:28s} {v / args.steps:9.3f} ms", file=sys.stderr)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rate, sample = cpu_baseline(D, A)
-        cpu = {"value": rate, "unit": "factor·asset·days/s", "cores": 1, "kind": "port", "sample": sample}
 
     if rank == 0:
         line = {
@@ -229,15 +317,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY 8(d) generator, device-generated)",
-            "config": {"workload": "C2 ops+IC+icir_top+corr-prune", "dates": D, "assets": A, "factors": F,
+            "config": {"workload": WORKLOAD_NAME[args.workload], "dates": D, "assets": A, "factors": F,
                        "parallelism": f"date-shard{world}", "sel_window": cfg.sel_window, "top_x": cfg.top_x},
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": bytes_per_unit(dom, F) * local_units, "ms": dom_ms},
+            "roofline": roofline,
             "stages_ms": {k: round(v / args.steps, 3) for k, v in stages.items()},
             "step_bytes_per_unit": step_bpu,
             "step_GBs": step_bpu * local_units / (ms_step * 1e-3) / 1e9,
             "cpu_baseline": cpu,
+            "reference_cpu": REFERENCE_CPU,
         }
         print(json.dumps(line))
     if world > 1:

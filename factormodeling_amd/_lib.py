@@ -42,6 +42,7 @@ SIGNATURES = {
     "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_zscore_exposures_range": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
@@ -51,6 +52,9 @@ SIGNATURES = {
     "fmx_wcomp_pct": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
     "fmx_wcomp_proxy": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
     "fmx_trade_equal": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_dbl, c_vp],
+    "fmx_trade_linear": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_dbl, c_vp],
+    "fmx_trade_books": [c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp],
+    "fmx_shift_rows": [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
     "fmx_mm_combine": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_pnl_daily": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],

@@ -51,51 +51,59 @@ def composite_factor_calculation(factors_df: pd.DataFrame, selected_factors: lis
     return pd.Series(vals, index=factors_df.index, name="composite_factor")
 
 
-def _weighted_plan(P, selection_df: pd.DataFrame, used: list):
-    """Per selection row: selected columns (selection_df column order), suffix codes,
-    prefix groups, group weights and pooled suffix column lists."""
-    col_of = {c: k for k, c in enumerate(used)}
-    rows = []
-    for date, weights in selection_df.iterrows():
-        today = weights[weights > 0].index.tolist()
-        d = P.dates.get_indexer([date])[0] if len(P.dates) else -1
-        if not today or d < 0:
-            rows.append((-1, [], [], [], []))
-            continue
-        groups = _prefix_groups(today)
-        gidx = {}
-        for g, (p, facs) in enumerate(groups.items()):
-            for k in facs:
-                gidx[k] = g
-        gw = [weights[[today[k] for k in facs]].sum() for facs in groups.values()]
-        gws = sum(gw)
-        gw = [x / gws for x in gw] if gws > 0 else [1 / len(gw)] * len(gw)
-        rows.append((int(d), [col_of[c] for c in today], [engine.suffix_code(c) for c in today],
-                     [gidx[k] for k in range(len(today))], gw))
-    J = len(rows)
-    KMAX = max([1] + [len(r[1]) for r in rows])
+def weighted_plan(pdate, W, names):
+    """Per selection row j (panel date index pdate[j], -1 = not a panel date; weights
+    W[j] over ``names`` in selection_df column order): the selected columns (w > 0, column
+    order), their suffix codes, prefix groups numbered by first appearance among them,
+    the group weights (composite_factor.py:276-290: sums in column order, normalised, or
+    equal when all zero) and the pooled suffix column lists (:251-268)."""
+    W = np.asarray(W, dtype=np.float64)
+    J, F = W.shape
+    suffix = np.array([engine.suffix_code(n) for n in names], dtype=np.int32)
+    pref = [n.split("_", 1)[0] for n in names]
+    sel = W > 0
+    KMAX = int(max(1, sel.sum(axis=1).max() if J else 1))
     col = np.zeros((J, KMAX), np.int32)
     suf = np.zeros((J, KMAX), np.int32)
     grp = np.full((J, KMAX), -1, np.int32)
     gwa = np.zeros((J, KMAX), np.float64)
     ncol = np.zeros(J, np.int32)
     ngrp = np.zeros(J, np.int32)
-    pdate = np.full(J, -1, np.int32)
+    pd_out = np.full(J, -1, np.int32)
     soff = [0]
     scol = []
-    for j, (d, cs, ss, gs, gw) in enumerate(rows):
-        pdate[j] = d
-        ncol[j] = len(cs)
-        ngrp[j] = len(gw)
-        col[j, :len(cs)] = cs
-        suf[j, :len(ss)] = ss
-        grp[j, :len(gs)] = gs
-        gwa[j, :len(gw)] = gw
-        for s in range(1, 5):
-            scol.extend(c for c, sc in zip(cs, ss) if sc == s)
+    for j in range(J):
+        cs = np.flatnonzero(sel[j]) if pdate[j] >= 0 else np.zeros(0, np.int64)
+        if cs.size:
+            gid, members, gs = {}, [], []
+            for c in cs:
+                g = gid.setdefault(pref[c], len(gid))
+                if g == len(members):
+                    members.append([])
+                members[g].append(c)
+                gs.append(g)
+            gsum = [W[j, m].sum() for m in members]   # pandas Series.sum = numpy sum (:281)
+            tot = sum(gsum)                           # Python sum (:282)
+            gw = [x / tot for x in gsum] if tot > 0 else [1 / len(gsum)] * len(gsum)
+            pd_out[j] = pdate[j]
+            ncol[j] = cs.size
+            ngrp[j] = len(gw)
+            col[j, :cs.size] = cs
+            suf[j, :cs.size] = suffix[cs]
+            grp[j, :cs.size] = gs
+            gwa[j, :len(gw)] = gw
+        for sc in range(1, 5):
+            scol.extend(int(c) for c in cs if suffix[c] == sc)
             soff.append(len(scol))
-    return {"pdate": pdate, "ncol": ncol, "col": col, "suf": suf, "grp": grp, "ngrp": ngrp, "gw": gwa,
+    return {"pdate": pd_out, "ncol": ncol, "col": col, "suf": suf, "grp": grp, "ngrp": ngrp, "gw": gwa,
             "KMAX": KMAX, "soff": np.asarray(soff, np.int32), "scol": np.asarray(scol or [0], np.int32)}
+
+
+def _weighted_plan(P, selection_df: pd.DataFrame, used: list):
+    """weighted_plan for a selection DataFrame restricted to the ``used`` columns."""
+    pdate = P.dates.get_indexer(selection_df.index) if len(P.dates) else np.full(len(selection_df), -1)
+    W = selection_df[used].to_numpy(dtype=np.float64) if used else np.zeros((len(selection_df), 0))
+    return weighted_plan(pdate, W, used)
 
 
 def weighted_composite_factor(factors_df: pd.DataFrame, selection_df: pd.DataFrame, method: str = "zscore") -> pd.Series:

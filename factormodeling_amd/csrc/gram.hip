@@ -33,14 +33,16 @@ constexpr int MKP = MK + 8;    // padded row (16 B)
 
 // per-date z-score of one (f, d) row; builder spec: mean/std(ddof=0) over non-NaN,
 // NaN -> 0, sigma in {0, NaN} -> whole row 0 and M = 0.  M is written as bf16 0/1.
+// Dates [d0, d0 + gridDim.x) of X [F][D][ld] into Z / M [F][Dout][ld] (Dout = the range
+// length: a date chunk of a panel too large to materialise Z for all dates).
 __global__ void __launch_bounds__(256)
 k_zscore_exposures(const double* __restrict__ X, double* __restrict__ Z, uint16_t* __restrict__ M, int64_t D,
-                   int64_t A, int64_t ld) {
+                   int64_t A, int64_t ld, int64_t d0, int64_t Dout) {
   __shared__ double dscr[16];
   const int64_t d = blockIdx.x, f = blockIdx.y;
-  const double* x = X + (f * D + d) * ld;
-  double* z = Z + (f * D + d) * ld;
-  uint16_t* m = M + (f * D + d) * ld;
+  const double* x = X + (f * D + d0 + d) * ld;
+  double* z = Z + (f * Dout + d) * ld;
+  uint16_t* m = M + (f * Dout + d) * ld;
   double s = 0.0, c = 0.0;
   for (int64_t a = threadIdx.x; a < A; a += 256) {
     double v = x[a];
@@ -542,7 +544,19 @@ extern "C" fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t*
   FMX_ARG(X && Z && M, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
   if (F == 0 || D == 0) return FMX_OK;
-  k_zscore_exposures<<<dim3((unsigned)D, (unsigned)F), 256, 0, as_stream(stream)>>>(X, Z, M, D, A, ld);
+  k_zscore_exposures<<<dim3((unsigned)D, (unsigned)F), 256, 0, as_stream(stream)>>>(X, Z, M, D, A, ld, 0, D);
+  FMX_LAUNCH_CHECK("k_zscore_exposures");
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D,
+                                                 int64_t A, int64_t ld, int64_t d0, int64_t d1, void* stream) {
+  FMX_ARG(X && Z && M, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d0 <= d1 && d1 <= D, "bad dims");
+  if (F == 0 || d1 == d0) return FMX_OK;
+  FMX_ARG(F <= 65535, "too many factors");
+  k_zscore_exposures<<<dim3((unsigned)(d1 - d0), (unsigned)F), 256, 0, as_stream(stream)>>>(X, Z, M, D, A, ld, d0,
+                                                                                            d1 - d0);
   FMX_LAUNCH_CHECK("k_zscore_exposures");
   return FMX_OK;
 }

@@ -24,13 +24,18 @@ constexpr int SIM_BLOCK = 256;
 
 __global__ void __launch_bounds__(SIM_BLOCK)
 k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
-              double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double pct) {
+              double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double pct,
+              int nan_absent) {
   extern __shared__ double sx[];  // [A]
   __shared__ int s_npos, s_nneg, s_npres;
   __shared__ unsigned s_hist[512];
   __shared__ uint64_t s_prefix[2], s_mask[2];
   __shared__ unsigned s_krem[2];
-  const int64_t d = blockIdx.x;
+  const int64_t d = blockIdx.x, mgr = blockIdx.y;   // managers batched along y
+  X += mgr * D * A;
+  W += mgr * D * A;
+  if (Wshift) Wshift += mgr * D * A;
+  counts += mgr * D * 2;
   const double* x = X + d * A;
   const uint8_t* p = present ? present + d * A : nullptr;
   double* w = W + d * A;
@@ -38,7 +43,8 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   __syncthreads();
   int np = 0, nn = 0, npr = 0;
   for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
-    const bool pr = !p || p[a];
+    // nan_absent: a NaN cell is no row (multi_manager.py:44 feeds factors_df[fac].dropna())
+    const bool pr = (!p || p[a]) && (!nan_absent || x[a] == x[a]);
     npr += pr;
     const double v = pr ? x[a] : __builtin_nan("");
     sx[a] = v;
@@ -121,7 +127,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
     const double v = sx[a];
     double out = 0.0;
-    if (p && !p[a]) {
+    if ((p && !p[a]) || (nan_absent && v != v)) {
       out = __builtin_nan("");
     } else if (!flat && (v > 0.0 || v < 0.0)) {
       const bool lg = v > 0.0;
@@ -155,6 +161,8 @@ constexpr int SHIFT_SEG = 64;
 __global__ void k_shift_rows(const double* __restrict__ W, double* __restrict__ out, int64_t D, int64_t A) {
   const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= A) return;
+  W += (int64_t)blockIdx.z * D * A;               // managers batched along z
+  out += (int64_t)blockIdx.z * D * A;
   const int64_t d0 = (int64_t)blockIdx.y * SHIFT_SEG;
   const int64_t d1 = d0 + SHIFT_SEG < D ? d0 + SHIFT_SEG : D;
   double last = __builtin_nan("");
@@ -263,13 +271,17 @@ template <int EMAX>
 __global__ void __launch_bounds__(LIN_NT)
 k_trade_linear(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
                double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double mw,
-               PwTable pw) {
+               PwTable pw, int nan_absent) {
   extern __shared__ double sub[];                 // [A] compacted subset
   __shared__ double nodes[2 * (16384 / 64) + 8];
   __shared__ int iscr[LIN_NW + 2];
   __shared__ int wtot[EMAX * LIN_NW + 1];
   const int t = threadIdx.x;
-  const int64_t d = blockIdx.x;
+  const int64_t d = blockIdx.x, mgr = blockIdx.y;   // managers batched along y
+  X += mgr * D * A;
+  W += mgr * D * A;
+  if (Wshift) Wshift += mgr * D * A;
+  counts += mgr * D * 2;
   const double* x = X + d * A;
   const uint8_t* p = present ? present + d * A : nullptr;
   double w[EMAX];
@@ -277,8 +289,9 @@ k_trade_linear(const double* __restrict__ X, const uint8_t* __restrict__ present
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     const int64_t a = t + (int64_t)k * LIN_NT;
-    const bool pr = a < A && (!p || p[a]);
-    const double v = pr ? x[a] : 0.0;
+    const double xv = a < A ? x[a] : 0.0;
+    const bool pr = a < A && (!p || p[a]) && (!nan_absent || xv == xv);
+    const double v = pr ? xv : 0.0;
     pm |= (uint32_t)pr << k;
     fpos |= (uint32_t)(pr && v > 0.0) << k;
     fneg |= (uint32_t)(pr && v < 0.0) << k;
@@ -508,33 +521,6 @@ k_daily_corr(const double* __restrict__ X, const double* __restrict__ R, double*
 
 using namespace fmx;
 
-extern "C" fmx_status fmx_trade_linear(const double* X, const uint8_t* present, double* Wraw, double* Wout,
-                                       double* counts, int64_t D, int64_t A, double max_weight, void* stream) {
-  FMX_ARG(X && Wraw && Wout && counts && D >= 0 && A >= 0, "bad args");
-  FMX_ARG(Wraw != Wout && Wraw != X, "Wraw must not alias X or Wout");
-  FMX_ARG(A <= 16384, "trade list holds one date row per workgroup: A <= 16384");
-  if (D == 0 || A == 0) return FMX_OK;
-  FMX_ARG(D <= 0x7fffffffll, "too many dates");
-  fmx_status e = FMX_OK;
-  PwTable pw = pw_table((int)A, &e);
-  if (e) return e;
-  const int E = (int)ceil_div(A, LIN_NT);
-  const void* k = E <= 1 ? (const void*)k_trade_linear<1> : E <= 2 ? (const void*)k_trade_linear<2>
-                : E <= 4 ? (const void*)k_trade_linear<4> : E <= 8 ? (const void*)k_trade_linear<8>
-                           : (const void*)k_trade_linear<16>;
-  const size_t lds = (size_t)A * sizeof(double);
-  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  double* ws = present ? nullptr : Wout;
-  void* args[] = {(void*)&X, (void*)&present, (void*)&Wraw, (void*)&ws, (void*)&counts, (void*)&D, (void*)&A,
-                  (void*)&max_weight, (void*)&pw};
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D), dim3(LIN_NT), args, lds, as_stream(stream)));
-  if (!present) return FMX_OK;
-  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG));
-  k_shift_rows<<<g, 256, 0, as_stream(stream)>>>(Wraw, Wout, D, A);
-  FMX_LAUNCH_CHECK("k_shift_rows");
-  return FMX_OK;
-}
-
 extern "C" fmx_status fmx_pnl_daily(const double* W, const double* R, const double* CAP, const int32_t* wprev,
                                     double* out, double* contrib, int64_t D, int64_t A, void* stream) {
   FMX_ARG(W && R && wprev && out && D >= 0 && A >= 0, "bad args");
@@ -559,25 +545,71 @@ extern "C" fmx_status fmx_daily_corr(const double* X, const double* R, double* o
   return FMX_OK;
 }
 
-extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
-                                      double* counts, int64_t D, int64_t A, double pct, void* stream) {
-  FMX_ARG(X && Wraw && Wout && counts && D >= 0 && A >= 0, "bad args");
+// Trade books of F managers [F][D][A] (F = 1: one signal), method 0 = equal, 1 = linear.
+static fmx_status trade_book(int method, const double* X, const uint8_t* present, int nan_absent, double* Wraw,
+                             double* Wout, double* counts, int64_t F, int64_t D, int64_t A, double pct, double mw,
+                             hipStream_t st) {
+  FMX_ARG(X && Wraw && Wout && counts && F >= 0 && D >= 0 && A >= 0, "bad args");
   FMX_ARG(Wraw != Wout && Wraw != X, "Wraw must not alias X or Wout");
-  FMX_ARG(A <= 16384, "trade list stages one date row in LDS: A <= 16384");
+  FMX_ARG(A <= 16384, "trade list holds one date row per workgroup: A <= 16384");
   FMX_ARG(pct >= 0.0, "pct must be >= 0");
-  if (D == 0 || A == 0) return FMX_OK;
+  FMX_ARG(F <= 65535 && D <= 0x7fffffffll, "too many managers / dates");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  const bool ragged = present || nan_absent;
+  double* ws = ragged ? nullptr : Wout;             // dense: the kernel writes the shifted book
   const size_t lds = (size_t)A * sizeof(double);
-  if (lds > 64 * 1024)
-    FMX_HIP(hipFuncSetAttribute((const void*)k_trade_equal, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  // dense: the kernel writes the shifted book too; ragged: shift over each symbol's rows
-  k_trade_equal<<<(unsigned)D, SIM_BLOCK, lds, as_stream(stream)>>>(X, present, Wraw, present ? nullptr : Wout,
-                                                                    counts, D, A, pct);
-  FMX_LAUNCH_CHECK("k_trade_equal");
-  if (!present) return FMX_OK;
-  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG));
-  k_shift_rows<<<g, 256, 0, as_stream(stream)>>>(Wraw, Wout, D, A);
+  if (method == 0) {
+    if (lds > 64 * 1024)
+      FMX_HIP(hipFuncSetAttribute((const void*)k_trade_equal, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_trade_equal<<<dim3((unsigned)D, (unsigned)F), SIM_BLOCK, lds, st>>>(X, present, Wraw, ws, counts, D, A, pct,
+                                                                           nan_absent);
+    FMX_LAUNCH_CHECK("k_trade_equal");
+  } else {
+    fmx_status e = FMX_OK;
+    PwTable pw = pw_table((int)A, &e);
+    if (e) return e;
+    const int E = (int)ceil_div(A, LIN_NT);
+    const void* k = E <= 1 ? (const void*)k_trade_linear<1> : E <= 2 ? (const void*)k_trade_linear<2>
+                  : E <= 4 ? (const void*)k_trade_linear<4> : E <= 8 ? (const void*)k_trade_linear<8>
+                             : (const void*)k_trade_linear<16>;
+    if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    void* args[] = {(void*)&X, (void*)&present, (void*)&Wraw, (void*)&ws, (void*)&counts, (void*)&D, (void*)&A,
+                    (void*)&mw, (void*)&pw, (void*)&nan_absent};
+    FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(LIN_NT), args, lds, st));
+  }
+  if (!ragged) return FMX_OK;
+  // ragged: shift over each manager's own rows (present cells are never NaN in its book)
+  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG), (unsigned)F);
+  k_shift_rows<<<g, 256, 0, st>>>(Wraw, Wout, D, A);
   FMX_LAUNCH_CHECK("k_shift_rows");
   return FMX_OK;
+}
+
+extern "C" fmx_status fmx_shift_rows(const double* W, double* out, int64_t F, int64_t D, int64_t A, void* stream) {
+  FMX_ARG(W && out && W != out && F >= 0 && D >= 0 && A >= 0 && F <= 65535, "bad args");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  dim3 g((unsigned)ceil_div(A, 256), (unsigned)ceil_div(D, SHIFT_SEG), (unsigned)F);
+  k_shift_rows<<<g, 256, 0, as_stream(stream)>>>(W, out, D, A);
+  FMX_LAUNCH_CHECK("k_shift_rows");
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
+                                      double* counts, int64_t D, int64_t A, double pct, void* stream) {
+  return trade_book(0, X, present, 0, Wraw, Wout, counts, 1, D, A, pct, 0.0, as_stream(stream));
+}
+
+extern "C" fmx_status fmx_trade_linear(const double* X, const uint8_t* present, double* Wraw, double* Wout,
+                                       double* counts, int64_t D, int64_t A, double max_weight, void* stream) {
+  return trade_book(1, X, present, 0, Wraw, Wout, counts, 1, D, A, 0.0, max_weight, as_stream(stream));
+}
+
+extern "C" fmx_status fmx_trade_books(int32_t method, const double* X, const uint8_t* present, int32_t nan_absent,
+                                      double* Wraw, double* Wout, double* counts, int64_t F, int64_t D, int64_t A,
+                                      double pct, double max_weight, void* stream) {
+  FMX_ARG(method == 0 || method == 1, "method must be 0 (equal) or 1 (linear)");
+  return trade_book(method, X, present, nan_absent, Wraw, Wout, counts, F, D, A, pct, max_weight,
+                    as_stream(stream));
 }
 
 extern "C" fmx_status fmx_mm_combine(const double* Wf, const double* counts, const double* fw, const int32_t* colmap,

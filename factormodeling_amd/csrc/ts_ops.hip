@@ -442,6 +442,116 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
   }
 }
 
+// Dense panels, windows without a register ring (W not instantiated in k_ts_reg, e.g. the
+// C5 window of 60): the moment machines only need the value LEAVING the window, which on
+// a dense panel is x[d - W] -- re-read from memory instead of kept in a ring (a 60-deep
+// LDS ring would hold one wave per 30 KB of LDS).  One lane per (factor, asset) column,
+// PF dates of both streams in flight; same state machines and operation order as
+// ts_step, so the outputs are bit-identical.  OP in {SUM, MEAN, STD, VAR, ZSCORE}.
+template <int OP, int PF>
+__global__ void __launch_bounds__(256)
+k_ts_rl(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld, int W) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  ColState c;
+  c.init();
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double v[PF], o[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      v[q] = d < D ? x[d * ld] : 0.0;
+      o[q] = (d < D && d >= W) ? x[(d - W) * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      const double vv = v[q];
+      if (c.first) { c.ss.init(vv); c.ms.init(vv); c.vs.init(vv); c.first = false; }
+      const bool full = c.i >= W;
+      double out;
+      if (OP == FMX_TS_SUM) {
+        if (full) c.ss.remove(o[q]);
+        c.ss.add(vv);
+        out = c.ss.result(W);
+      } else if (OP == FMX_TS_MEAN) {
+        if (full) c.ms.remove(o[q]);
+        c.ms.add(vv);
+        out = c.ms.result(W);
+      } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
+        if (full) c.vs.remove(o[q]);
+        c.vs.add(vv);
+        const double var = c.vs.var(W, 1);
+        out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
+      } else {  // ZSCORE
+        if (full) { c.ms.remove(o[q]); c.vs.remove(o[q]); }
+        c.ms.add(vv); c.vs.add(vv);
+        const double m = c.ms.result(W);
+        double sd = zsqrt(c.vs.var(W, 1));
+        if (sd == 0.0) sd = qnan();
+        out = (vv - m) / sd;
+      }
+      y[d * ld] = out;
+      c.i += 1;
+    }
+  }
+}
+
+// ts_corr on dense panels with the leaving values re-read (k_ts_corr's ring is 2W x 64
+// doubles of LDS per wave).  Same operation order as k_ts_corr: bit-identical.
+template <int PF>
+__global__ void __launch_bounds__(256)
+k_ts_corr_rl(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ Out, int64_t F,
+             int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  const double* yc = Ycol + f * y_fstride + a;
+  double* o = Out + f * D * ld + a;
+  MeanSt mxy, mx, my;
+  VarSt vx, vy;
+  int64_t i = 0, cnt = 0;
+  bool first = true;
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double xr[PF], yr[PF], xo[PF], yo[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      xr[q] = d < D ? x[d * ld] : 0.0;
+      yr[q] = d < D ? yc[d * ld] : 0.0;
+      const bool old = d < D && d >= W;
+      xo[q] = old ? x[(d - W) * ld] : 0.0;
+      yo[q] = old ? yc[(d - W) * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      const double xv = xr[q] + 0.0 * yr[q];
+      const double yv = yr[q] + 0.0 * xr[q];
+      const double pv = xv * yv;
+      if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; }
+      if (i >= W) {
+        const double ox = xo[q] + 0.0 * yo[q], oy = yo[q] + 0.0 * xo[q];
+        mxy.remove(ox * oy); mx.remove(ox); my.remove(oy); vx.remove(ox); vy.remove(oy);
+        cnt -= (ox + oy == ox + oy);
+      }
+      mxy.add(pv); mx.add(xv); my.add(yv); vx.add(xv); vy.add(yv);
+      cnt += (xv + yv == xv + yv);
+      const double cc = (double)cnt;
+      const double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (cc / (cc - 1.0));
+      const double den = sqrt(vx.var(W, 1) * vy.var(W, 1));
+      o[d * ld] = num / den;
+      i += 1;
+    }
+  }
+}
+
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // One lane owns V adjacent assets of one factor (V = 2: 16-byte loads/stores) and walks
@@ -733,6 +843,17 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
       FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, st));
       return FMX_OK;
     }
+    // other windows: the leaving value is re-read instead of kept in a ring
+    const void* kl = op == FMX_TS_SUM ? (const void*)k_ts_rl<FMX_TS_SUM, 8>
+                   : op == FMX_TS_MEAN ? (const void*)k_ts_rl<FMX_TS_MEAN, 8>
+                   : op == FMX_TS_STD ? (const void*)k_ts_rl<FMX_TS_STD, 8>
+                   : op == FMX_TS_VAR ? (const void*)k_ts_rl<FMX_TS_VAR, 8>
+                   : op == FMX_TS_ZSCORE ? (const void*)k_ts_rl<FMX_TS_ZSCORE, 8> : nullptr;
+    if (kl && W >= 1) {
+      void* rargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W};
+      FMX_HIP(hipLaunchKernel(kl, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, st));
+      return FMX_OK;
+    }
   }
   size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * V * sizeof(double);
   const void* k = nullptr;
@@ -787,6 +908,13 @@ extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* O
   FMX_ARG(window >= 1, "window must be >= 1");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   int W = window;
+  if (!present && getenv("FMX_TS_LDS") == nullptr) {   // dense: leaving values re-read
+    void* rargs[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
+                     (void*)&y_fstride, (void*)&W};
+    FMX_HIP(hipLaunchKernel((const void*)k_ts_corr_rl<4>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0,
+                            as_stream(stream)));
+    return FMX_OK;
+  }
   dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
   size_t lds = (size_t)2 * W * TS_BLOCK * sizeof(double);
   void* args[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,

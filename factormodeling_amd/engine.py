@@ -74,7 +74,7 @@ def ts_set(X, outs: dict, window: int, rank_window: int, present=None):
     return outs
 
 
-def ts_corr(X, Ycol, window: int, present=None):
+def ts_corr(X, Ycol, window: int, present=None, out=None):
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
@@ -88,7 +88,7 @@ def ts_corr(X, Ycol, window: int, present=None):
             raise _lib.FmxError("Ycol must be [D][A] or [F][D][A]")
         ystride = D * A
     Ycol = Ycol.contiguous()
-    out = torch.empty_like(X)
+    out = _out(X, out)
     call("fmx_ts_corr", ptr(X), ptr(Ycol), ptr(out), F, D, A, A, ystride, int(window), ptr(present), stream_ptr())
     return out
 
@@ -294,6 +294,34 @@ def gram_fused(X, stats, d0=0, d1=None):
     return G, N
 
 
+GRAM_CHUNK_BYTES = 8 << 30      # Z + M workspace of one date chunk of the wide Gram
+
+
+def gram_chunked(X, d0=0, d1=None, chunk=None):
+    """G, N over dates [d0, d1) for wide factor sets (F > 256, e.g. C4's 2000): Z / M are
+    materialised one date chunk at a time (fmx_zscore_exposures_range, <= GRAM_CHUNK_BYTES)
+    and accumulated into G / N by the tiled fp64 / bf16 MFMA kernels in chunk order
+    (deterministic), so the panel never needs a full-size Z next to it."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    d1 = D if d1 is None else d1
+    if chunk is None:
+        chunk = max(1, min(d1 - d0, int(GRAM_CHUNK_BYTES // max(1, F * A * 10))))
+    G = torch.zeros((F, F), dtype=F64, device=X.device)
+    N = torch.zeros((F, F), dtype=F64, device=X.device)
+    Z = M = None
+    for c0 in range(d0, d1, chunk):
+        c1 = min(d1, c0 + chunk)
+        n = c1 - c0
+        if Z is None or Z.shape[1] != n:
+            Z = torch.empty((F, n, A), dtype=F64, device=X.device)
+            M = torch.empty((F, n, A), dtype=torch.bfloat16, device=X.device)
+        call("fmx_zscore_exposures_range", ptr(X), ptr(Z), ptr(M), F, D, A, A, c0, c1, stream_ptr())
+        call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, n, A, A, 0, n, 1, stream_ptr())
+    return G, N
+
+
 def corr_matrix(X, d0=0, d1=None, stats=None):
     """Builder-defined factor correlation: C = G / N on fp64 MFMA.  F <= 256
     takes the fused path (row stats from cs_moment, one pass over X); wider panels
@@ -304,8 +332,7 @@ def corr_matrix(X, d0=0, d1=None, stats=None):
             _, stats = cs_moment_stats("stats", X)
         G, N = gram_fused(X, stats, d0, d1)
     else:
-        Z, M = zscore_exposures(X)
-        G, N = gram(Z, M, d0, d1)
+        G, N = gram_chunked(X, d0, d1)
     return torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
 
 
@@ -438,6 +465,49 @@ def trade_equal(X, pct: float, present=None):
     call("fmx_trade_equal", ptr(X), ptr(present), ptr(Wraw), ptr(Wout), ptr(counts), D, A, float(pct),
          stream_ptr())
     return Wout, counts
+
+
+def trade_linear(X, max_weight: float, present=None):
+    """Simulation._daily_trade_list, method 'linear' (portfolio_simulation.py:172-181,
+    :250-313) on one [D][A] panel: (shifted weights [D][A], counts [D][2])."""
+    if X.dim() != 2 or X.dtype != F64 or not X.is_cuda:
+        raise _lib.FmxError("X must be a float64 [D][A] device tensor")
+    X = X.contiguous()
+    D, A = X.shape
+    _check_present(present, D, A)
+    Wraw, Wout = torch.empty_like(X), torch.empty_like(X)
+    counts = torch.empty((D, 2), dtype=F64, device=X.device)
+    call("fmx_trade_linear", ptr(X), ptr(present), ptr(Wraw), ptr(Wout), ptr(counts), D, A, float(max_weight),
+         stream_ptr())
+    return Wout, counts
+
+
+TRADE_METHODS = {"equal": 0, "linear": 1}
+
+
+def trade_books(X, method: str, pct=0.1, max_weight=0.03, present=None, nan_absent=True, raw=False):
+    """F trade books in one launch (fmx_trade_books): X [F][D][A] -> (shifted [F][D][A],
+    counts [F][D][2]) (+ the same-day books with ``raw``); with nan_absent a NaN cell is no row."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    _check_present(present, D, A)
+    if method not in TRADE_METHODS:
+        raise NotImplementedError(f"method {method!r}: the device runs 'equal' and 'linear'")
+    Wraw, Wout = torch.empty_like(X), torch.empty_like(X)
+    counts = torch.empty((F, D, 2), dtype=F64, device=X.device)
+    call("fmx_trade_books", TRADE_METHODS[method], ptr(X), ptr(present), int(bool(nan_absent)), ptr(Wraw),
+         ptr(Wout), ptr(counts), F, D, A, float(pct), float(max_weight), stream_ptr())
+    return (Wout, counts, Wraw) if raw else (Wout, counts)
+
+
+def shift_rows(W):
+    """Per-symbol shift(1) over each book's present (non-NaN) rows (fmx_shift_rows)."""
+    W = as3(W).contiguous()
+    F, D, A = W.shape
+    out = torch.empty_like(W)
+    call("fmx_shift_rows", ptr(W), ptr(out), F, D, A, stream_ptr())
+    return out
 
 
 def mm_combine(Wf, counts, fw, colmap, wdate):

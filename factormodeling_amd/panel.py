@@ -56,6 +56,22 @@ class PanelIndex:
             self.present_np = None
         self._present_dev = {}
 
+    def row_layout(self):
+        """(pos, width, sorted_within): every row's position inside its date in INPUT order
+        (the order a ``groupby('date')`` group presents its rows), the widest date, and
+        whether that order is the sorted-symbol order on every date.  Per-date reductions
+        whose rounding depends on row order (numpy pairwise sums) run on this layout."""
+        order = np.argsort(self.d, kind="stable")
+        dd = self.d[order]
+        starts = np.searchsorted(dd, np.arange(self.D))
+        pos = np.empty(self.n, dtype=np.int64)
+        pos[order] = np.arange(self.n) - starts[dd]
+        width = int(np.bincount(self.d, minlength=self.D).max()) if self.n else 0
+        ss = self.s[order]
+        same = dd[1:] == dd[:-1]
+        sorted_within = not bool(np.any(same & (ss[1:] <= ss[:-1])))
+        return pos, width, sorted_within
+
     # ------------------------------------------------------------------ host <-> dense
     def to_dense(self, values: np.ndarray) -> np.ndarray:
         """values [n] or [n][F] (row order) -> dense [F][D][A] (NaN where absent)."""

@@ -33,12 +33,50 @@ HALO = MAX_LOOKBACK - 1 + 2  # rolling warm-up + IC lag 2
 
 @dataclass
 class StepConfig:
+    """One benchmark step.  Defaults = C2 (BASELINE configs[1]); ``workload_config`` gives
+    C4 (wide factor zoo: IC order + chunked 2000 x 2000 Gram + greedy prune) and C5
+    (ts_corr / ts_std at 60 days over factor chunks, rolling-IC icir_top weights, weighted
+    composite)."""
     sel_window: int = SEL_WINDOW
     top_x: int = 5
     icir_threshold: float = -1.0
     prune_rho: float = 0.7
     ops: list = field(default_factory=lambda: list(OPS))
     fuse: bool = True          # multi-output kernels: one read of X for several operators
+    ic_lags: tuple = (1, 2)
+    select: bool = True        # rolling-window metrics + icir_top per processed day
+    gram: bool = True          # correlation Gram + greedy pruning
+    prune_top_x: object = "top_x"   # None: prune the whole ordered zoo
+    ret_ops: list = field(default_factory=list)   # [(op, window)] vs returns: ("corr", 60), ("std", 60)
+    factor_chunk: int = 0      # ret_ops run over chunks of this many factors (memory)
+    composite: object = None   # "zscore" | "rank": weighted composite of the day's selection
+    names: object = None       # factor names (composite suffix / prefix rules)
+
+    @property
+    def lookback(self):
+        w = [o[2] for o in self.ops if o[2]] + [w for _, w in self.ret_ops]
+        return max(w) if w else 1
+
+    @property
+    def halo(self):
+        return self.lookback - 1 + max(self.ic_lags)
+
+
+def factor_names(F):
+    """SURVEY 8(d) generator names: g{f//4:03d}_{f:04d}_{suffix}, suffixes cycling."""
+    suf = ["eq", "flx", "long", "short", "raw"]
+    return [f"g{f // 4:03d}_{f:04d}_{suf[f % 5]}" for f in range(F)]
+
+
+def workload_config(name):
+    if name == "c2":
+        return StepConfig()
+    if name == "c4":
+        return StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None)
+    if name == "c5":
+        return StepConfig(ops=[], ic_lags=(1, 2), select=True, gram=False, ret_ops=[("corr", 60), ("std", 60)],
+                          factor_chunk=100, composite="zscore")
+    raise ValueError(f"unknown workload {name!r}")
 
 
 def _op_key(kind, op, w):
@@ -118,12 +156,14 @@ class ShardedPanel:
     dates, stored contiguously as X[F][halo + own][A]."""
 
     def __init__(self, D, A, F, rank, world, device, seed=0, halo=HALO):
+        # halo: rolling warm-up + IC lag of the step's longest window (StepConfig.halo)
         self.D, self.A, self.F = D, A, F
         self.rank, self.world = rank, world
         per = (D + world - 1) // world
         self.d_lo = min(D, rank * per)
         self.d_hi = min(D, (rank + 1) * per)
         self.halo = halo if rank > 0 else 0
+        self.halo_len = halo
         self.device = device
         Xo, Ro, lo = synthetic_panel(D, A, F, device, seed, self.d_lo, self.d_hi, 0)
         assert lo == self.d_lo
@@ -144,7 +184,7 @@ class ShardedPanel:
         (RCCL point-to-point over xGMI; gloo on CPU)."""
         if self.world == 1:
             return
-        H = HALO
+        H = self.halo_len
         reqs = []
         if self.rank + 1 < self.world:
             send_x = self.X[:, -H:].contiguous()
@@ -208,9 +248,13 @@ class EngineBackend:
             if stats is None:
                 _, stats = E.cs_moment_stats("stats", X)
             return E.gram_fused(X, stats, d0, d1)
-        Z, M = E.zscore_exposures(X[:, d0:d1].contiguous())
-        return E.gram(Z, M)
+        return E.gram_chunked(X, d0, d1)
 
+    @staticmethod
+    def ts_corr_into(X, R, w, out):
+        E.ts_corr(X, R, w, out=out)
+
+    wcomp = staticmethod(E.wcomp)
     ic_daily = staticmethod(E.ic_daily)
     ic_window = staticmethod(E.ic_window)
     select_icir_top = staticmethod(E.select_icir_top)
@@ -273,23 +317,55 @@ def _rec(timers, name, t0):
     timers.append((name, t0, e))
 
 
+def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
+    """Operators against the returns (C5: ts_corr(x, R, w), plus ts_std(x, w)) over factor
+    chunks of ``cfg.factor_chunk`` into reused buffers (a full-size output per operator
+    would not fit next to a 100 GB panel)."""
+    F = sp.X.shape[0]
+    fc = cfg.factor_chunk or F
+    bufs = getattr(sp, "ret_bufs", None)
+    if bufs is None or bufs[0].shape[0] != min(fc, F):
+        bufs = [torch.empty((min(fc, F),) + tuple(sp.X.shape[1:]), dtype=sp.X.dtype, device=sp.X.device)
+                for _ in cfg.ret_ops]
+        sp.ret_bufs = bufs
+    for f0 in range(0, F, fc):
+        f1 = min(F, f0 + fc)
+        Xc = sp.X[f0:f1]
+        for (op, w), buf in zip(cfg.ret_ops, bufs):
+            out = buf[: f1 - f0]
+            t0 = _ev(timers)
+            if op == "corr":
+                be.ts_corr_into(Xc, sp.R, w, out)
+            else:
+                be.op("ts", op, w, Xc, out)
+            _rec(timers, f"ret:{op}:{w}", t0)
+            if collect is not None:
+                collect.setdefault(f"ret:{op}:{w}", []).append(out[:, sp.halo:].clone())
+
+
 def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=None):
     """One pass of the hot path.  Returns (selected weights [J][F] (every rank holds the
-    full result), kept factor list).  ``collect`` (tests) receives intermediate results."""
+    full result; None without selection), kept factor list (None without the Gram)).
+    ``collect`` (tests) receives intermediate results."""
     t0 = _ev(timers)
     sp.exchange_halo()
     _rec(timers, "halo", t0)
     side = {}
-    sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                      own=slice(sp.halo, None), side=side)
-    # daily IC at lags 1 and 2 for owned dates (halo provides the lagged rows)
+    if cfg.ops:
+        sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                          own=slice(sp.halo, None), side=side)
+    if cfg.ret_ops:
+        run_ret_ops(sp, cfg, timers, be, collect)
+    # daily IC for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
-    daily = be.ic_daily(sp.X, sp.R, (1, 2))[:, :, :, sp.halo:]          # [2][4][F][own]
+    lags = tuple(cfg.ic_lags)
+    daily = be.ic_daily(sp.X, sp.R, lags)[:, :, :, sp.halo:]          # [L][4][F][own]
     _rec(timers, "ic_daily", t0)
     t0 = _ev(timers)
+    L = len(lags)
     if sp.world > 1:
         per = (sp.D + sp.world - 1) // sp.world
-        pad = torch.zeros((2, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
+        pad = torch.zeros((L, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
         pad[..., :daily.shape[3]] = daily
         parts = [torch.empty_like(pad) for _ in range(sp.world)]
         dist.all_gather(parts, pad)
@@ -299,31 +375,57 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     _rec(timers, "allgather_ic", t0)
     t0 = _ev(timers)
     D = full.shape[3]
-    W = cfg.sel_window
-    proc = list(range(W, D - 1))
     summ = be.ic_window(full[0].contiguous(), [0], [D])                # full-sample metrics
-    win = be.ic_window(full[1].contiguous(), [i - W + 1 for i in proc], proc)
-    order, w = be.select_icir_top(win, True, cfg.icir_threshold, cfg.top_x)
+    w = win = None
+    if cfg.select:
+        W = cfg.sel_window
+        proc = list(range(W, D - 1))
+        win = be.ic_window(full[L - 1].contiguous(), [i - W + 1 for i in proc], proc)
+        order, w = be.select_icir_top(win, True, cfg.icir_threshold, cfg.top_x)
     _rec(timers, "select", t0)
-    # correlation Gram over owned dates, all-reduced
-    t0 = _ev(timers)
-    if hasattr(be, "corr_gram"):
-        G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
-    else:
-        Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
-        G, N = be.gram(Z, M)
-    if sp.world > 1:
-        G, N = ordered_sum(G, sp.world), ordered_sum(N, sp.world)
-    C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
-    _rec(timers, "gram", t0)
-    t0 = _ev(timers)
-    rir = summ[0, :, 3]
-    full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
-    kept = be.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, cfg.top_x)
-    _rec(timers, "prune", t0)
+    comp = None
+    if cfg.composite and w is not None:
+        t0 = _ev(timers)
+        comp = weighted_composite_step(sp, cfg, w, be)
+        _rec(timers, "composite", t0)
+    kept = C = None
+    if cfg.gram:
+        # correlation Gram over owned dates, summed over ranks in rank order
+        t0 = _ev(timers)
+        if hasattr(be, "corr_gram"):
+            G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
+        else:
+            Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
+            G, N = be.gram(Z, M)
+        if sp.world > 1:
+            G, N = ordered_sum(G, sp.world), ordered_sum(N, sp.world)
+        C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
+        _rec(timers, "gram", t0)
+        t0 = _ev(timers)
+        rir = summ[0, :, 3]
+        full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
+        top = cfg.top_x if cfg.prune_top_x == "top_x" else cfg.prune_top_x
+        kept = be.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, top)
+        _rec(timers, "prune", t0)
     if collect is not None:
-        collect.update(daily=full, summ=summ, win=win, C=C)
+        collect.update(daily=full, summ=summ, win=win, C=C, comp=comp)
     return w, kept
+
+
+def weighted_composite_step(sp, cfg, w, be=ENGINE):
+    """weighted_composite_factor (composite_factor.py:220-342) of each processed day's
+    selection over this rank's owned dates: the day's selected columns, pooled suffix
+    percentiles, prefix proxies, group weights, z-score / rank, demeaning."""
+    from .composite_factor import weighted_plan
+    W = cfg.sel_window
+    D = w.shape[0] + W + 1
+    proc = np.arange(W, D - 1)
+    local = proc - sp.d_lo + sp.halo                    # rows of the local panel
+    own = (proc >= sp.d_lo) & (proc < sp.d_hi)
+    pdate = np.where(own, local, -1)
+    names = cfg.names or factor_names(sp.F)
+    plan = weighted_plan(pdate, w.cpu().numpy(), names)
+    return be.wcomp(sp.X, plan, cfg.composite)
 
 
 def ordered_sum(T, world):

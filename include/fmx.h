@@ -184,6 +184,10 @@ fmx_status fmx_select_icir_top(const double* metrics, int64_t J, int64_t F, int3
  * 0/1 (uint16 bit patterns [F][D][ld]). */
 fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
                                 int64_t ld, void* stream);
+/* fmx_zscore_exposures for the dates [d0, d1) only: Z / M are [F][d1 - d0][ld] (chunked
+ * Gram of a panel whose full Z / M would not fit next to X, e.g. C4 at 121 GB). */
+fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
+                                      int64_t ld, int64_t d0, int64_t d1, void* stream);
 /* G[F][F] (+)= sum_{d in [d0,d1), a} Z[i][d][a] Z[j][d][a] on fp64 MFMA
  * (v_mfma_f64_16x16x4_f64) and N[F][F] (+)= the same sum over M on bf16 MFMA (exact
  * pair counts).  accumulate = 0 overwrites.  M/N may be NULL. */
@@ -231,6 +235,23 @@ fmx_status fmx_wcomp_combine(const double* Nrm, const int32_t* pdate, const int3
  * with no present row.  A <= 16384. */
 fmx_status fmx_trade_equal(const double* X, const uint8_t* present, double* Wraw, double* Wout,
                            double* counts, int64_t D, int64_t A, double pct, void* stream);
+/* Method 'linear' (portfolio_simulation.py:172-181): the signal on its positive / negative
+ * cells, _normalize_legs (:250-262) and _cap_and_redistribute(max_weight, 10, 1e-6)
+ * (:264-313), every pandas sum a numpy pairwise sum over its subset in symbol order
+ * (bit-identical); counts = (len(pos), len(neg)).  Same layout as fmx_trade_equal. */
+fmx_status fmx_trade_linear(const double* X, const uint8_t* present, double* Wraw, double* Wout,
+                            double* counts, int64_t D, int64_t A, double max_weight, void* stream);
+/* F trade books in one launch (multi_manager.py:41-49: one manager per factor): X, Wraw,
+ * Wout [F][D][A], counts [F][D][2]; method 0 = equal (pct), 1 = linear (max_weight);
+ * present [D][A] shared (or NULL); nan_absent = 1 treats NaN cells as no row
+ * (factors_df[fac].dropna()). */
+fmx_status fmx_trade_books(int32_t method, const double* X, const uint8_t* present, int32_t nan_absent,
+                           double* Wraw, double* Wout, double* counts, int64_t F, int64_t D, int64_t A,
+                           double pct, double max_weight, void* stream);
+/* Per-symbol shift(1) over the present rows of F same-day books W [F][D][A] (present
+ * cells are never NaN in a book, absent ones always are): out[f][d][a] = the book's value
+ * on the symbol's previous present row (portfolio_simulation.py:151-152). */
+fmx_status fmx_shift_rows(const double* W, double* out, int64_t F, int64_t D, int64_t A, void* stream);
 /* Replaces multi_manager.compute_multimanager_weights' combination loop (:51-72): Wf
  * [F][D][A] shifted manager books and counts [F][D][2] (NaN on dates a manager has no
  * rows) from fmx_trade_equal; fw [Dw][Fw] factor weights, colmap [Fw] column -> manager

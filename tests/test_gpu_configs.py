@@ -239,3 +239,67 @@ def test_factor_selector_ragged(dev, prefix):
         ref = merge_dups(st[f"out_{key}__vals"], ref_cols, canon)
         assert np.array_equal(got > 0, ref > 0), key
         assert_close(got.ravel(), ref.ravel(), rtol=1e-12, atol=0, what=key)
+
+
+def test_gram_chunked_dates_vs_oracle(dev):
+    """The wide Gram accumulated over date chunks (C4 memory plan) equals the oracle."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(43)
+    F, D, A = 300, 7, 90
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    X[4, 2] = 0.5                                   # constant row -> excluded
+    Xd = torch.as_tensor(X, device=dev)
+    for chunk in (1, 3, 7):
+        G, N = E.gram_chunked(Xd, 1, 6, chunk=chunk)
+        C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G)).cpu().numpy()
+        np.testing.assert_allclose(C, OG.corr_matrix(X, 1, 6), rtol=1e-10, atol=1e-12, err_msg=str(chunk))
+
+
+@pytest.mark.parametrize("W", [7, 37, 60])
+def test_ring_free_rolling_moments_vs_oracle(dev, W):
+    """Dense panels at windows without a register ring re-read the value leaving the
+    window (k_ts_rl): bit-identical to the oracle (pandas' add/remove machines)."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.ops as O
+    rng = np.random.default_rng(W)
+    X = rng.standard_normal((2, 150, 300))
+    X = np.where(rng.random(X.shape) < 0.1, np.round(X, 1), X)
+    X[rng.random(X.shape) < 0.02] = np.nan
+    X[0, 20:120, 5] = 0.3                           # constant run
+    Xd = torch.as_tensor(X, device=dev)
+    for op, fn in (("sum", O.ts_sum), ("mean", O.ts_mean), ("std", O.ts_std), ("zscore", O.ts_zscore)):
+        got = E.ts(op, Xd, W).cpu().numpy()
+        for f in range(2):
+            with np.errstate(all="ignore"):
+                ref = fn(X[f], W)
+            assert_close(got[f].ravel(), ref.ravel(), exact=True, what=f"{op}{W}")
+
+
+def test_c5_step_vs_oracle(dev):
+    """The C5 step at a reduced size: ts_corr(x, R, w) / ts_std(w) over factor chunks,
+    rolling-IC icir_top weights and the weighted composite of each day's selection."""
+    import torch
+    from factormodeling_amd import pipeline as PL
+    import oracle.composite as OC
+    import oracle.ops as O
+    D, A, F = 90, 300, 12
+    cfg = PL.workload_config("c5")
+    cfg.sel_window, cfg.factor_chunk, cfg.ret_ops = 20, 5, [("corr", 15), ("std", 15)]
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=9, halo=cfg.halo)
+    col = {}
+    w, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    X, R = sp.X.cpu().numpy(), sp.R.cpu().numpy()
+    corr = torch.cat(col["ret:corr:15"]).cpu().numpy()
+    std = torch.cat(col["ret:std:15"]).cpu().numpy()
+    for f in range(F):
+        assert_close(corr[f].ravel(), O.ts_corr(X[f], R, 15).ravel(), exact=True, what="c5 ts_corr")
+        assert_close(std[f].ravel(), O.ts_std(X[f], 15).ravel(), exact=True, what="c5 ts_std")
+    W = w.cpu().numpy()
+    ref = OC.weighted_composite_factor(X, PL.factor_names(F), list(range(20, D - 1)), W, "zscore")
+    assert_close(col["comp"].cpu().numpy().ravel(), ref.ravel(), rtol=RTOL, atol=ATOL, what="c5 composite")
+    assert kept is None
