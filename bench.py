@@ -40,24 +40,27 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFS = 78.6           # MI355X fp64 (vector = matrix) spec
 
 # algorithmic bytes per factor·asset·day: a unary operator reads X once and
-# writes once (16 B); the fused IC stage reads X once plus two R rows per (f, date) (8 + 16/F)
-def bytes_per_unit(stage, F):
+# writes once (16 B); the fused IC stage reads X once plus two R rows per (f, date) (8 + 16/F),
+# plus the 4-B ranks when it starts from the operator set's ranks (which the rank pass writes)
+def bytes_per_unit(stage, F, ranked=False):
     kind = stage.split(":")[0]
     if kind in ("ts", "cs_rank", "cs", "winsor"):
         return 16.0
     if kind == "ts_set":            # X once + five outputs (mean, std, zscore, rank, decay)
         return 48.0
-    if kind in ("cs_zscore_neutralize", "cs_rank_winsor"):   # X once + two outputs
+    if kind == "cs_zscore_neutralize":  # X once + two outputs
         return 24.0
+    if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u32)
+        return 28.0 if ranked else 24.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
         return 16.0
-    if kind == "ic_daily":
-        return 8.0 + 16.0 / F
+    if kind == "ic_daily":              # X once (+ its u32 ranks when ranked) + two R rows
+        return (12.0 if ranked else 8.0) + 16.0 / F
     return None
 
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
-STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
+STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_ranked<", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
                 "ts_set": "fmx::k_ts_set<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
@@ -280,16 +283,18 @@ def main():
 
     # dominant kernel: the slowest HBM-priced stage (one launch of one kernel per step),
     # timed with HIP events recorded on the launch stream inside the timed steps
-    op_stages = {k: v / args.steps for k, v in stages.items() if bytes_per_unit(k, F) is not None}
+    ranked = getattr(sp, "rank2", None) is not None   # the IC started from the rank pass's ranks
+    bpu = lambda k: bytes_per_unit(k, F, ranked)      # noqa: E731
+    op_stages = {k: v / args.steps for k, v in stages.items() if bpu(k) is not None}
     dom, dom_ms = max(op_stages.items(), key=lambda kv: kv[1])
     local_units = float(F) * (sp.X.shape[1]) * A
-    achieved = bytes_per_unit(dom, F) * local_units / (dom_ms * 1e-3) / 1e9
+    achieved = bpu(dom) * local_units / (dom_ms * 1e-3) / 1e9
     # whole-step algorithmic bytes per unit of the HBM-priced stages (+ the Gram's X read)
-    step_bpu = sum(bytes_per_unit(k, F) for k in op_stages) + (8.0 if cfg.gram else 0.0)
+    step_bpu = sum(bpu(k) for k in op_stages) + (8.0 if cfg.gram else 0.0)
     traffic = pmc_traffic(dom, [sp.X.shape[1], A, F]) if world == 1 else None
     roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "algorithmic_bytes": bytes_per_unit(dom, F) * local_units, "ms": dom_ms}
+                "algorithmic_bytes": bpu(dom) * local_units, "ms": dom_ms}
     gram_ms = stages.get("gram", 0.0) / args.steps
     if cfg.gram and gram_ms > dom_ms:
         # the Gram dominates (C4): priced on MFMA -- the upper triangle incl. the diagonal of

@@ -30,7 +30,7 @@ SIGNATURES = {
     "fmx_cs_moment": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
     "fmx_cs_moment_stats": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_zscore_neutralize": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
-    "fmx_cs_rank_winsor": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
+    "fmx_cs_rank_winsor": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
     "fmx_cs_filter_center": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
@@ -39,9 +39,12 @@ SIGNATURES = {
     "fmx_elementwise": [c_i32, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_vp],
     "fmx_bucket": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "fmx_ic_daily": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "fmx_ic_daily_ranked": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
     "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_corr_prune_windows": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32,
+                               c_dbl, c_dbl, c_i32, c_vp, c_vp],
     "fmx_zscore_exposures_range": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],

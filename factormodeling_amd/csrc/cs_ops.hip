@@ -482,6 +482,20 @@ k_group(const double* __restrict__ X, const int32_t* __restrict__ G, double* __r
       for (int p = s + threadIdx.x; p < e; p += CS_NT) nvl += keys[p] < KEY_SENTINEL - 1;
       int nvv;
       block_exscan<CS_NT>(nvl, iscr, &nvv);
+      if (method == FMX_RANK_DENSE && nvv > 1) {
+        // dense rank = #distinct keys <= k among the group's valid members (chunked scan)
+        const int C = (nvv + CS_NT - 1) / CS_NT, p0 = s + threadIdx.x * C, p1 = min(s + nvv, p0 + C);
+        int c = 0;
+        for (int p = p0; p < p1; ++p) c += (p == s || keys[p] != keys[p - 1]);
+        int tot;
+        int base = block_exscan<CS_NT>(c, iscr, &tot);
+        for (int p = p0; p < p1; ++p) {
+          base += (p == s || keys[p] != keys[p - 1]);
+          y[idx[p]] = ((double)base - 1.0) / (double)(nvv - 1);
+        }
+        for (int p = s + nvv + threadIdx.x; p < e; p += CS_NT) y[idx[p]] = qnan();
+        continue;
+      }
       for (int p = s + threadIdx.x; p < e; p += CS_NT) {
         int a = idx[p];
         if (nvv <= 1) { y[a] = 0.5; continue; }
@@ -777,13 +791,15 @@ extern "C" fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64
 
 extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D,
                                          int64_t A, int64_t ld, double qlo, double qhi, const uint8_t* present,
-                                         void* stream) {
+                                         uint32_t* rank2, void* stream) {
   FMX_ARG(X && Yrank && Ywinsor, "null panel");
   FMX_ARG(Yrank != X && Ywinsor != X && Yrank != Ywinsor, "outputs must be distinct from X and each other");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(!(rank2 && present), "rank2 ranks every non-NaN cell: no presence mask");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
-  fmx_status e = br_cs_rank_winsor(X, Yrank, Ywinsor, F, D, A, ld, qlo, qhi, present, as_stream(stream));
+  fmx_status e = br_cs_rank_winsor(X, Yrank, Ywinsor, F, D, A, ld, qlo, qhi, present, rank2, as_stream(stream));
   if (e != FMX_ERR_UNSUPPORTED) return e;
+  if (rank2) { set_error("rank2 needs the fused rank kernel (A <= 16384)"); return FMX_ERR_UNSUPPORTED; }
   // rows the fused kernel does not take: the two single-op passes
   if ((e = fmx_cs_rank(X, Yrank, F, D, A, ld, FMX_RANK_AVERAGE, present, stream))) return e;
   return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
@@ -793,6 +809,172 @@ extern "C" fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F
                                            int64_t ld, double qlo, double qhi, const uint8_t* present,
                                            void* stream) {
   return cs_quantile(1, X, Y, F, D, A, ld, qlo, qhi, present, stream);
+}
+
+// ------------------------------------------------------------------------------------
+// Group ops on long rows (k_group sorts the whole row in LDS: A <= 4096).  One 1024-thread
+// workgroup per (date, factor) row keeps its cells in registers (cell t + k*GL_NT) and
+// visits the groups one at a time: the group's members are compacted in asset order
+// (ballot prefix per register chunk) into LDS and reduced with the numpy pairwise schedule
+// of their count (the reference's x.mean() over the group's rows), then every owner
+// writes its cells.  Rank: the group's (key, asset) pairs are bitonic-sorted in LDS and
+// each owner binary-searches its key ('first': its (key, asset) pair; 'dense': the
+// distinct-value prefix written over the sorted asset slots).
+constexpr int GL_NT = 1024;
+constexpr int GL_NW = GL_NT / 64;
+
+template <int EMAX>
+__device__ int gl_offsets(uint32_t flags, int* pre, int* wtot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const uint64_t b = __ballot((flags >> k) & 1u);
+    pre[k] = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[k * GL_NW + wid] = __popcll(b);
+  }
+  __syncthreads();
+  if (wid == 0) {
+    constexpr int N = EMAX * GL_NW, PER = (N + 63) / 64;
+    int loc[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { const int i = lane * PER + j; loc[j] = i < N ? wtot[i] : 0; sum += loc[j]; }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(incl, o, 64); if (lane >= o) incl += u; }
+    int run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { const int i = lane * PER + j; if (i < N) wtot[i] = run; run += loc[j]; }
+    if (lane == 63) wtot[N] = incl;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) pre[k] += wtot[k * GL_NW + wid];
+  return wtot[EMAX * GL_NW];
+}
+
+template <int OP, int EMAX>
+__global__ void __launch_bounds__(GL_NT)
+k_group_long(const double* __restrict__ X, const int32_t* __restrict__ G, double* __restrict__ Y, int64_t D,
+             int64_t A, int64_t ld, int ngroups, int method, const uint8_t* __restrict__ present, PwTable pw,
+             int Pmax) {
+  extern __shared__ uint64_t gl[];                // [Pmax] values / keys, then [Pmax] u16 asset slots
+  __shared__ double nodes[2 * (16384 / 64) + 8];
+  __shared__ int iscr[GL_NW + 2];
+  __shared__ int wtot[EMAX * GL_NW + 1];
+  const int t = threadIdx.x;
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d) * ld;
+  const int32_t* g = G + d * ld;
+  double* y = Y + (f * D + d) * ld;
+  const uint8_t* prow = present ? present + d * ld : nullptr;
+  double xv[EMAX];
+  int gv[EMAX];
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int64_t a = t + (int64_t)k * GL_NT;
+    const bool in = a < A && (!prow || prow[a]);
+    xv[k] = a < A ? x[a] : 0.0;
+    gv[k] = in ? g[a] : -1;
+    if (a < A && gv[k] < 0) y[a] = qnan();       // absent row or NaN group
+  }
+  uint16_t* slot = (uint16_t*)(gl + Pmax);
+  for (int gg = 0; gg < ngroups; ++gg) {
+    uint32_t fl = 0;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) fl |= (uint32_t)(gv[k] == gg) << k;
+    int pre[EMAX];
+    const int m = gl_offsets<EMAX>(fl, pre, wtot);
+    if (m == 0) continue;                         // block-uniform
+    if (OP != 3) {
+      double* vals = reinterpret_cast<double*>(gl);
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k)
+        if ((fl >> k) & 1u) vals[pre[k]] = xv[k];
+      __syncthreads();
+      const int32_t* sch = pw.get(m);
+      int cnt;
+      const double s1 = block_pw_sum_w0<GL_NT>([&](int i) { const double v = vals[i]; return v == v ? v : 0.0; },
+                                               [&](int i) { return (int)(vals[i] == vals[i]); }, sch, nodes, iscr,
+                                               &cnt);
+      const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+      double sd = 0.0;
+      if (OP == 2) {
+        int c2;
+        const double s2 = block_pw_sum_w0<GL_NT>([&](int i) {
+          const double v = vals[i];
+          const double z = v == v ? v : 0.0;
+          const double q = (mean - z) * (mean - z);
+          return v == v ? q : 0.0;
+        }, [](int) { return 0; }, sch, nodes, iscr, &c2);
+        sd = sqrt(cnt > 0 ? s2 / (double)cnt : qnan());
+      }
+      const bool guard = (OP == 2) && (sd == 0.0 || sd != sd);
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        if (!((fl >> k) & 1u)) continue;
+        const double v = xv[k];
+        double o;
+        if (OP == 0) o = mean;
+        else if (OP == 1) o = v - mean;
+        else o = guard ? 0.0 : (v - mean) / sd;
+        y[t + (int64_t)k * GL_NT] = o;
+      }
+    } else {
+      int P = 2;
+      while (P < m) P <<= 1;
+      if (P > Pmax) {                             // group larger than the sort buffer
+#pragma unroll
+        for (int k = 0; k < EMAX; ++k)
+          if ((fl >> k) & 1u) y[t + (int64_t)k * GL_NT] = qnan();
+        __syncthreads();
+        continue;
+      }
+      uint64_t* keys = gl;
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        if (!((fl >> k) & 1u)) continue;
+        const double v = xv[k];
+        keys[pre[k]] = v == v ? okey(v) : KEY_SENTINEL - 1;   // NaN members sort last
+        slot[pre[k]] = (uint16_t)(t + k * GL_NT);
+      }
+      for (int i = m + t; i < P; i += GL_NT) { keys[i] = KEY_SENTINEL; slot[i] = 0xffff; }
+      __syncthreads();
+      bitonic_sort<GL_NT>(keys, slot, P);
+      const int nvv = lower_bound_u64(keys, 0, m, KEY_SENTINEL - 1);
+      if (method == FMX_RANK_DENSE && nvv > 1) {
+        // dense rank of every sorted position, written over the (unused) asset slots
+        const int C = (nvv + GL_NT - 1) / GL_NT, p0 = t * C, p1 = min(nvv, p0 + C);
+        int c = 0;
+        for (int p = p0; p < p1; ++p) c += (p == 0 || keys[p] != keys[p - 1]);
+        int tot;
+        int base = block_exscan<GL_NT>(c, iscr, &tot);
+        for (int p = p0; p < p1; ++p) { base += (p == 0 || keys[p] != keys[p - 1]); slot[p] = (uint16_t)base; }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        if (!((fl >> k) & 1u)) continue;
+        const double v = xv[k];
+        const int64_t a = t + (int64_t)k * GL_NT;
+        if (nvv <= 1) { y[a] = 0.5; continue; }
+        if (!(v == v)) { y[a] = qnan(); continue; }
+        const uint64_t kk = okey(v);
+        const int less = lower_bound_u64(keys, 0, nvv, kk);
+        const int eq = upper_bound_u64(keys, less, nvv, kk) - less;
+        double r;
+        if (method == FMX_RANK_MIN) r = (double)(less + 1);
+        else if (method == FMX_RANK_MAX) r = (double)(less + eq);
+        else if (method == FMX_RANK_DENSE) r = (double)slot[less];
+        else if (method == FMX_RANK_FIRST) {
+          int lo = less, hi = less + eq;              // ties sorted by asset
+          while (lo < hi) { const int md = (lo + hi) >> 1; if (slot[md] < (uint16_t)a) lo = md + 1; else hi = md; }
+          r = (double)(lo + 1);
+        } else r = (double)less + (double)(eq + 1) / 2.0;
+        y[a] = (r - 1.0) / (double)(nvv - 1);
+      }
+    }
+    __syncthreads();                              // LDS reused by the next group
+  }
 }
 
 extern "C" fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F,
@@ -806,6 +988,27 @@ extern "C" fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G
   fmx_status e = FMX_OK;
   PwTable pw = pw_table((int)A, &e);
   if (e) return e;
+  if (A > 4096 && getenv("FMX_GROUP_SORTED") == nullptr) {
+    // long rows: per-group compaction (moments) / per-group sort (rank) in one LDS buffer
+    FMX_ARG(A <= 16384, "group ops hold one row in registers: A <= 16384");
+    // rank: (key, asset) pairs of the largest group, sorted in LDS (<= 8192 members)
+    int P = 2;
+    while (P < A) P <<= 1;
+    int Pmax = op == FMX_GROUP_RANK ? std::min(P, 8192) : (int)A;
+    const size_t lds = op == FMX_GROUP_RANK ? (size_t)Pmax * 10 + 64 : (size_t)A * 8 + 64;
+    const int E = (int)ceil_div(A, GL_NT);
+#define FMX_GL(O) (E <= 5 ? (const void*)k_group_long<O, 5> : E <= 8 ? (const void*)k_group_long<O, 8> \
+                           : E <= 12 ? (const void*)k_group_long<O, 12> : (const void*)k_group_long<O, 16>)
+    const void* kl = op == FMX_GROUP_MEAN ? FMX_GL(0) : op == FMX_GROUP_NEUTRALIZE ? FMX_GL(1)
+                   : op == FMX_GROUP_NORMALIZE ? FMX_GL(2) : FMX_GL(3);
+#undef FMX_GL
+    if ((e = set_lds(kl, lds))) return e;
+    int ng = ngroups, m = method;
+    void* args[] = {(void*)&X, (void*)&G, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&ng, (void*)&m,
+                    (void*)&present, (void*)&pw, (void*)&Pmax};
+    FMX_HIP(hipLaunchKernel(kl, dim3((unsigned)D, (unsigned)F), dim3(GL_NT), args, lds, as_stream(stream)));
+    return FMX_OK;
+  }
   int P = next_pow2((int)A);
   if (P < 2) P = 2;
   size_t lds = (size_t)P * 12 + 16 + (size_t)P * 8 + (2 * (P / 64) + 8) * 8 + 16 * 4 + (ngroups + 1) * 4 + 64;

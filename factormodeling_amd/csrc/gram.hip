@@ -513,6 +513,94 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   return FMX_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Rolling correlation pruning (the builder-defined corr_prune selector, SURVEY A19, run for
+// every processed day of FactorSelector): window j pools the per-date Gram partials of the
+// raw dates [s0[j], s0[j] + W) -- the lag-1 factors of the window's dates -- and walks the
+// day's metrics order (rank_IC_IR / IC_IR descending): a candidate above the threshold is
+// kept iff |G(f,k) / N(f,k)| < rho for every kept k (0 where N = 0), up to top_x.  One
+// wave per window; lane i sums the W partials of kept factor i in date order.
+__global__ void __launch_bounds__(64)
+k_window_prune(const double* __restrict__ partG, const double* __restrict__ partN, int FP, int64_t F, int64_t d_lo,
+               int64_t nd, int W, const int32_t* __restrict__ s0, const int32_t* __restrict__ order,
+               const double* __restrict__ metrics, int col, double thr, double rho, int top_x,
+               double* __restrict__ w_out) {
+  extern __shared__ int kept[];                   // [F]
+  const int64_t j = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int32_t* ord = order + j * F;
+  const double* m = metrics + j * F * 8;
+  const int64_t a0 = max<int64_t>((int64_t)s0[j], d_lo), a1 = min<int64_t>((int64_t)s0[j] + W, d_lo + nd);
+  int nk = 0;
+  for (int64_t pos = 0; pos < F && nk < top_x; ++pos) {
+    const int f = ord[pos];
+    const double v = m[(int64_t)f * 8 + col];
+    if (!(v > thr)) continue;                     // NaN fails (factor_selection_methods.py:14 analogue)
+    bool ok = true;
+    for (int base = 0; base < nk && ok; base += 64) {
+      bool bad = false;
+      const int i = base + lane;
+      if (i < nk) {
+        const int k = kept[i];
+        const int r = min(f, k), c = max(f, k);
+        double g = 0.0, n = 0.0;
+        for (int64_t d = a0; d < a1; ++d) {
+          const int64_t off = (d - d_lo) * (int64_t)FP * FP + (int64_t)r * FP + c;
+          g += partG[off];
+          n += partN[off];
+        }
+        const double cc = n > 0.0 ? g / n : 0.0;
+        bad = !(fabs(cc) < rho);
+      }
+      ok = __ballot(bad) == 0;
+    }
+    if (ok) {
+      if (lane == 0) kept[nk] = f;
+      ++nk;
+      __syncthreads();
+    }
+  }
+  double* w = w_out + j * F;
+  for (int64_t f = lane; f < F; f += 64) w[f] = 0.0;
+  __syncthreads();
+  for (int i = lane; i < nk; i += 64) w[kept[i]] = 1.0 / (double)nk;
+}
+
+template <int NB>
+static fmx_status window_prune_launch(const double* X, const double* stats, int64_t F, int64_t D, int64_t A,
+                                      int64_t ld, int64_t J, int W, const int32_t* s0_host, const int32_t* order,
+                                      const double* metrics, int col, double thr, double rho, int top_x,
+                                      double* w_out, hipStream_t st) {
+  constexpr int FP = 16 * NB;
+  int64_t d_lo = D, d_hi = 0;
+  for (int64_t j = 0; j < J; ++j) {
+    d_lo = std::min<int64_t>(d_lo, std::max<int64_t>(0, s0_host[j]));
+    d_hi = std::max<int64_t>(d_hi, std::min<int64_t>(D, (int64_t)s0_host[j] + W));
+  }
+  if (d_hi <= d_lo) d_hi = d_lo = 0;
+  const int64_t nd = d_hi - d_lo;
+  double* part = nullptr;
+  int32_t* s0 = nullptr;
+  FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * std::max<int64_t>(nd, 1) * FP * FP, st));
+  FMX_HIP(hipMallocAsync((void**)&s0, sizeof(int32_t) * J, st));
+  FMX_HIP(hipMemcpyAsync(s0, s0_host, sizeof(int32_t) * J, hipMemcpyHostToDevice, st));
+  if (nd > 0) {
+    // one slice per date: the partials ARE the per-date Grams (G on fp64 MFMA, N on bf16)
+    k_gram_small<NB, 0><<<(unsigned)nd, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d_lo, d_hi, 1, part, nullptr);
+    FMX_LAUNCH_CHECK("k_gram_small<G>");
+    k_gram_small<NB, 1><<<(unsigned)nd, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d_lo, d_hi, 1,
+                                                        part + nd * FP * FP, nullptr);
+    FMX_LAUNCH_CHECK("k_gram_small<N>");
+  }
+  k_window_prune<<<(unsigned)J, 64, sizeof(int) * F, st>>>(part, part + nd * FP * FP, FP, F, d_lo, nd, W, s0, order,
+                                                          metrics, col, thr, rho, top_x, w_out);
+  FMX_LAUNCH_CHECK("k_window_prune");
+  FMX_HIP(hipFreeAsync(part, st));
+  FMX_HIP(hipFreeAsync(s0, st));
+  FMX_HIP(hipStreamSynchronize(st));              // s0_host may be a temporary
+  return FMX_OK;
+}
+
 }  // namespace fmx
 
 using namespace fmx;
@@ -615,4 +703,32 @@ extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, do
   fmx_status e = gram_run(Z, false, G, F, D, A, ld, d0, d1, accumulate, st);
   if (e || !M || !N) return e;
   return gram_run(M, true, N, F, D, A, ld, d0, d1, accumulate, st);
+}
+
+extern "C" fmx_status fmx_corr_prune_windows(const double* X, const double* stats, int64_t F, int64_t D, int64_t A,
+                                             int64_t ld, int64_t J, int32_t window, const int32_t* s0_host,
+                                             const int32_t* order, const double* metrics, int32_t use_rank_icir,
+                                             double threshold, double rho, int32_t top_x, double* w_out,
+                                             void* stream) {
+  FMX_ARG(X && stats && s0_host && order && metrics && w_out, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && J >= 0 && window >= 1 && top_x >= 0, "bad dims");
+  if (F > 256) {
+    set_error("fmx_corr_prune_windows keeps per-date F x F partials: F <= 256");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  if (F == 0 || J == 0) return FMX_OK;
+  FMX_ARG(J <= 0x7fffffffll, "too many windows");
+  hipStream_t st = as_stream(stream);
+  const int col = use_rank_icir ? 3 : 1;
+  const int nb = (int)ceil_div(F, 16);
+  switch (nb) {
+#define FMX_WP(K)                                                                                            \
+  case K:                                                                                                    \
+    return window_prune_launch<K>(X, stats, F, D, A, ld, J, window, s0_host, order, metrics, col, threshold, \
+                                  rho, top_x, w_out, st);
+    FMX_WP(1) FMX_WP(2) FMX_WP(3) FMX_WP(4) FMX_WP(5) FMX_WP(6) FMX_WP(7) FMX_WP(8)
+    FMX_WP(9) FMX_WP(10) FMX_WP(11) FMX_WP(12) FMX_WP(13) FMX_WP(14) FMX_WP(15) FMX_WP(16)
+#undef FMX_WP
+    default: return FMX_ERR_UNSUPPORTED;
+  }
 }

@@ -318,6 +318,17 @@ extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, 
   return FMX_OK;
 }
 
+extern "C" fmx_status fmx_ic_daily_ranked(const double* X, const uint32_t* rank2, const double* R, int64_t F,
+                                          int64_t D, int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags,
+                                          double* out, void* stream) {
+  FMX_ARG(X && rank2 && R && out && lags, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
+  FMX_ARG(n_lags >= 1 && n_lags <= 8, "n_lags");
+  for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
+  if (F == 0 || D == 0) return FMX_OK;
+  return br_ic_ranked(X, rank2, R, F, D, A, ld, lags, n_lags, out, as_stream(stream));
+}
+
 extern "C" fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev,
                                     const int32_t* d1_dev, int64_t J, double* out, void* stream) {
   FMX_ARG(daily && d0_dev && d1_dev && out, "null pointer");

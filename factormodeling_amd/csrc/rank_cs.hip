@@ -26,8 +26,9 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   }
   double* Y2 = nullptr;
   double qlo = 0.0, qhi = 0.0;
+  uint32_t* RK = nullptr;
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
@@ -35,10 +36,11 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   return FMX_OK;
 }
 
-// cs_rank (method average) and cs_winsor of the same rows in one pass (k_cs_rank_fa<WQ>);
-// returns FMX_ERR_UNSUPPORTED when the row does not fit the fine kernel (caller splits).
+// cs_rank (method average) and cs_winsor of the same rows in one pass (k_cs_rank_fa<WQ>),
+// optionally the doubled ranks RK; returns FMX_ERR_UNSUPPORTED when the row does not fit
+// the fine kernel (caller splits).
 fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
-                             double qlo, double qhi, const uint8_t* present, hipStream_t st) {
+                             double qlo, double qhi, const uint8_t* present, uint32_t* RK, hipStream_t st) {
   const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
@@ -48,7 +50,7 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   if (F * D == 0) return FMX_OK;
   int method = FMX_RANK_AVERAGE;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi};
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;

@@ -43,10 +43,15 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 // The four numpy 'linear' order statistics are read off the ranks: after the in-bucket
 // scan every element knows #less / #equal among the valid keys, so the owner of order
 // statistic k (less <= k < less + equal) publishes its key -- no second pass over the row.
+//
+// RK (optional): 2 * average rank among the row's valid keys, i.e. 2*#less + #equal + 1
+// (0 for NaN / absent), as uint32 -- the daily IC of the same rows starts from it
+// (k_ic_ranked) instead of ranking them again.
 template <int NT, int EMAX, bool PRES, bool WQ = false>
 __global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
-             const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi) {
+             const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
+             uint32_t* __restrict__ RK) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
@@ -108,6 +113,11 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 #pragma unroll
     for (int k = 0; k < EMAX; ++k)
       if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+    if (RK) {                                 // nv == 0 or a single-row date (rank 1)
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k)
+        if (k < EMAX - 1 || last_in) RK[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? 0u : 2u;
+    }
     if (WQ) {                                 // nv < 5: winsor is the identity
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
@@ -199,6 +209,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
     y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
+    if (RK) RK[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -413,6 +424,37 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
       o = (v < lo || v > hi) ? v : 0.0;
     }
     y[t + k * NT] = (PRES && !((pm >> k) & 1)) ? qnan() : o;
+  }
+}
+
+// Thread 0 of an IC workgroup: the (n, IC, rank IC, beta) records of source row s for its
+// active lags from the block totals (cst: -min / max of f and r per lag, fin: the seven
+// moment sums per lag).
+__device__ __forceinline__ void fr_ic_store(double* out, int64_t F, int64_t D, int64_t s, int64_t f,
+                                            const int* lagv, const bool* act, const double* n,
+                                            const double* cst, const double* fin) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    if (!act[m]) continue;
+    const int64_t td = s + lagv[m];
+    double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
+    const int64_t stp = F * D;
+    const double nn = n[m];
+    double ic = qnan(), ric = qnan(), beta = qnan();
+    if (nn >= 3.0) {
+      const double* w = fin + 8 * m;
+      const bool fconst = (-cst[4 * m + 0]) == cst[4 * m + 1];
+      const bool rconst = (-cst[4 * m + 2]) == cst[4 * m + 3];
+      if (!fconst && !rconst) {
+        ic = fmin(1.0, fmax(-1.0, w[0] / sqrt(w[1] * w[2])));
+        ric = fmin(1.0, fmax(-1.0, w[3] / sqrt(w[4] * w[2])));
+      }
+      beta = w[5] > 0 ? w[6] / w[5] : qnan();
+    }
+    o[0] = nn;
+    o[stp] = ic;
+    o[2 * stp] = ric;
+    o[3 * stp] = beta;
   }
 }
 
@@ -666,32 +708,207 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
     if (t < 16) fin[t] = dscr[NW * 16 + t];
     __syncthreads();
   }
+  if (t == 0) fr_ic_store(out, F, D, s, f, lagv, act, n, cst, fin);
+  BR_PH();
+}
+
+// ------------------------------------------------------------------------------------
+// Daily IC from the ranks the cs_rank pass of the same panel already produced (RK =
+// 2*#less + #equal + 1 among the row's non-NaN exposures, k_cs_rank_fa), so no sort or
+// histogram is repeated.  The pairs of lag m are the non-NaN exposures minus E_m, those
+// whose lag-m return is NaN; the doubled pair rank is RK - (2*#less + #equal) over E_m.
+// E_m holds the row's NaN returns -- a few keys: gathered in LDS while the row loads,
+// sorted by one wave when <= 64 and binary-searched (#less + #less-or-equal is exactly
+// the correction); a longer E_m is gathered register-chunk by chunk and scanned.
+// Sums, moments and their reductions repeat k_ic_daily_fr step for step (same element
+// order, same butterflies), so the records are bit-identical to it.
+template <int NT, int EMAX>
+__global__ void __launch_bounds__(NT, (NT == 1024 && EMAX <= 5) ? 8 : 4)
+k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
+            int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out) {
+  constexpr int NW = NT / 64, ES = 64;
+  __shared__ double dscr[(NW + 1) * 16];
+  __shared__ uint64_t el[2][ES];              // E_m keys (first ES), then sorted
+  __shared__ uint64_t tb[NT];                 // long E_m: one register chunk's keys
+  __shared__ int ecnt[2], wcnt[NW];
+  __shared__ double cst[8], fin[16];
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int64_t s = blockIdx.x / F, f = blockIdx.x % F;
+  const double* xf = X + (f * D + s) * ld;
+  const uint32_t* rkf = RK + (f * D + s) * ld;
+  const int lagv[2] = {L0, L1};
+  const double* rr[2];
+  bool act[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    act[m] = m < NL && s + lagv[m] < D;
+    rr[m] = Rt + (act[m] ? s + lagv[m] : s) * ld;
+  }
+  if (!act[0] && !act[1]) return;
+  if (t < 2) ecnt[t] = 0;
+  double v1[4] = {0, 0, 0, 0};
+  double mx[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
+  int cw0 = 0, cw1 = 0;
+  const bool last_in = t + (EMAX - 1) * NT < A;
+  double xv[EMAX];
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) xv[k] = (k < EMAX - 1 || last_in) ? xf[t + k * NT] : qnan();
+  __syncthreads();                            // ecnt zeroed
+  uint32_t pm = 0, em = 0;                    // per element: pair / E mask of each lag
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int i = t + k * NT;
+    int mm = 0, ee = 0;
+    const double v = xv[k];
+    if (v == v) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        if (!act[m]) continue;
+        const double r = rr[m][i];
+        if (r != r) { ee |= 1 << m; continue; }
+        mm |= 1 << m;
+        v1[2 * m] += v;
+        v1[2 * m + 1] += r;
+        mx[4 * m + 0] = fmax(mx[4 * m + 0], -v);
+        mx[4 * m + 1] = fmax(mx[4 * m + 1], v);
+        mx[4 * m + 2] = fmax(mx[4 * m + 2], -r);
+        mx[4 * m + 3] = fmax(mx[4 * m + 3], r);
+      }
+      if (ee) {                               // rare: the row's NaN returns
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          if (!((ee >> m) & 1)) continue;
+          const int q = atomicAdd(&ecnt[m], 1);
+          if (q < ES) el[m][q] = okey(v);
+        }
+      }
+    }
+    pm |= (uint32_t)mm << (2 * k);
+    em |= (uint32_t)ee << (2 * k);
+    cw0 += __popcll(__ballot(mm & 1));
+    cw1 += __popcll(__ballot(mm & 2));
+  }
+  fr_part_bfly<4, false>(v1, dscr, 16, 0);
+  if ((t & 63) == 0) {
+    dscr[wid * 16 + 4] = (double)cw0;
+    dscr[wid * 16 + 5] = (double)cw1;
+    dscr[wid * 16 + 6] = 0.0;
+    dscr[wid * 16 + 7] = 0.0;
+  }
+  fr_part_bfly<8, true>(mx, dscr, 16, 8);
+  fr_fin_dpp<NT>(dscr, 16, 8);
+  const double* tot1 = dscr + NW * 16;
+  double tot[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) tot[q] = fr_uniform_d(tot1[q]);
   if (t == 0) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      if (!act[m]) continue;
-      const int64_t td = s + lagv[m];
-      double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
-      const int64_t stp = F * D;
-      const double nn = n[m];
-      double ic = qnan(), ric = qnan(), beta = qnan();
-      if (nn >= 3.0) {
-        const double* w = fin + 8 * m;
-        const bool fconst = (-cst[4 * m + 0]) == cst[4 * m + 1];
-        const bool rconst = (-cst[4 * m + 2]) == cst[4 * m + 3];
-        if (!fconst && !rconst) {
-          ic = fmin(1.0, fmax(-1.0, w[0] / sqrt(w[1] * w[2])));
-          ric = fmin(1.0, fmax(-1.0, w[3] / sqrt(w[4] * w[2])));
-        }
-        beta = w[5] > 0 ? w[6] / w[5] : qnan();
-      }
-      o[0] = nn;
-      o[stp] = ic;
-      o[2 * stp] = ric;
-      o[3 * stp] = beta;
-    }
+    for (int q = 0; q < 8; ++q) cst[q] = tot1[8 + q];
   }
-  BR_PH();
+  const double n[2] = {tot[4], tot[5]};
+  const bool need = (act[0] && n[0] >= 3.0) || (act[1] && n[1] >= 3.0);
+  if (need) {
+    // doubled ranks (loads in flight over the E sort)
+    uint32_t rk[EMAX];
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) rk[k] = (k < EMAX - 1 || last_in) ? rkf[t + k * NT] : 0u;
+    const int ne[2] = {__builtin_amdgcn_readfirstlane(ecnt[0]), __builtin_amdgcn_readfirstlane(ecnt[1])};
+    const int nw = wid == 0 ? ne[0] : ne[1];
+    if (wid < 2 && nw > 0 && nw <= ES) {
+      const uint64_t v = lane < nw ? el[wid][lane] : KEY_SENTINEL;
+      el[wid][lane] = wave_sort64(v, lane);
+    }
+    __syncthreads();
+    // cr[k] = doubled pair rank of lag 0 | lag 1 << 16: RK minus the E corrections (every
+    // partial difference stays >= the final one >= 2, so the fields never borrow)
+    uint32_t cr[EMAX];
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      cr[k] = rk[k] | (rk[k] << 16);
+      if (!((pm >> (2 * k)) & 3)) continue;
+      const uint64_t key = okey(xv[k]);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        if (!((pm >> (2 * k + m)) & 1) || ne[m] == 0 || ne[m] > ES) continue;
+        int lo = 0, le = 0;
+#pragma unroll
+        for (int st = ES / 2; st > 0; st >>= 1) {
+          lo += el[m][lo + st - 1] < key ? st : 0;
+          le += el[m][le + st - 1] <= key ? st : 0;
+        }
+        cr[k] -= (uint32_t)(lo + le) << (16 * m);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if (ne[m] <= ES) continue;
+      // long E_m: gather register chunk c's E members in asset order, scan them
+#pragma unroll 1
+      for (int c = 0; c < EMAX; ++c) {
+        const bool ex = (em >> (2 * c + m)) & 1;
+        const uint64_t b = __ballot(ex);
+        if (lane == 0) wcnt[wid] = __popcll(b);
+        __syncthreads();
+        int off = 0, tot_c = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int cw = wcnt[w];
+          off += w < wid ? cw : 0;
+          tot_c += cw;
+        }
+        if (ex) {
+          double xc = xv[0];
+#pragma unroll
+          for (int k = 1; k < EMAX; ++k) xc = c == k ? xv[k] : xc;
+          tb[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = okey(xc);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < EMAX; ++k) {
+          if (!((pm >> (2 * k + m)) & 1)) continue;
+          const uint64_t key = okey(xv[k]);
+          uint32_t a = 0;
+          for (int j = 0; j < tot_c; ++j) {
+            const uint64_t w = tb[j];
+            a += (w < key ? 1u : 0u) + (w <= key ? 1u : 0u);
+          }
+          cr[k] -= a << (16 * m);
+        }
+      }
+    }
+    double fm[2], rm[2], km[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const double dn = n[m];
+      fm[m] = tot[2 * m] / dn;
+      rm[m] = tot[2 * m + 1] / dn;
+      km[m] = (dn + 1.0) / 2.0;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      double w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        if (!((pm >> (2 * k + m)) & 1)) continue;
+        const int r2 = (int)((cr[k] >> (16 * m)) & 0xffff);
+        const int64_t i = t + (int64_t)k * NT;
+        const double fv = xv[k];
+        const double rkv = (double)r2 / 2.0;
+        const double r = rr[m][i];
+        const double dx = fv - fm[m], dy = r - rm[m], dk = rkv - km[m];
+        w[0] += dx * dy; w[1] += dx * dx; w[2] += dy * dy;
+        w[3] += dk * dy; w[4] += dk * dk;
+        w[5] += fv * fv; w[6] += fv * r;
+      }
+      fr_part_bfly<8, false>(w, dscr, 16, 8 * m);
+    }
+    fr_fin_dpp<NT>(dscr, 16, 16);
+    if (t < 16) fin[t] = dscr[NW * 16 + t];
+    __syncthreads();
+  }
+  if (t == 0) fr_ic_store(out, F, D, s, f, lagv, act, n, cst, fin);
 }
 
 }  // namespace fmx

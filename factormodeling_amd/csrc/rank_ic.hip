@@ -44,6 +44,25 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
   return FMX_OK;
 }
 
+// Daily IC from the doubled ranks of the same panel (k_ic_ranked): A <= 16384.
+fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
+                        int64_t ld, const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
+  const int nt = 1024;
+  if (br_emax(A, nt) < 0) { set_error("row too long for the ranked IC kernel (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
+  for (int base = 0; base < n_lags; base += 2) {
+    int NL = std::min(2, n_lags - base);
+    int L0 = lags_host[base], L1 = NL > 1 ? lags_host[base + 1] : 0;
+    double* o = out + (int64_t)base * 4 * F * D;
+    k_ic_empty<<<(unsigned)F, 64, 0, st>>>(o, F, D, L0, L1, NL);
+    FMX_LAUNCH_CHECK("k_ic_empty");
+    void* args[] = {(void*)&X, (void*)&RK, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,
+                    (void*)&L1, (void*)&NL, (void*)&o};
+    fmx_status e = launch_br(FMX_EMAX_TABLE(k_ic_ranked), nt, A, F * D, 0, args, st);
+    if (e) return e;
+  }
+  return FMX_OK;
+}
+
 }  // namespace fmx
 
 BR_PHASE_EXPORT(fmx_debug_phase_ic)

@@ -148,15 +148,23 @@ def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=Fal
     return (Yz, Yn, stats) if with_stats else (Yz, Yn)
 
 
-def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None):
-    """cs_rank(average) and cs_winsor(qlo, qhi) in one pass (fmx_cs_rank_winsor)."""
+RANKED_IC_MAX_A = 16384
+
+
+def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None, rank2=None):
+    """cs_rank(average) and cs_winsor(qlo, qhi) in one pass (fmx_cs_rank_winsor).
+    ``rank2`` (uint32 tensor shaped like X): also the doubled ranks that
+    ``ic_daily(..., rank2=)`` starts from."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
     _check_present(present, D, A)
     Yr, Yw = _out(X, out_rank), _out(X, out_winsor)
+    if rank2 is not None:
+        if rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+            raise _lib.FmxError("rank2 must be a contiguous int32 (bit pattern uint32) [F][D][A] tensor")
     call("fmx_cs_rank_winsor", ptr(X), ptr(Yr), ptr(Yw), F, D, A, A, float(qlo), float(qhi), ptr(present),
-         stream_ptr())
+         ptr(rank2), stream_ptr())
     return Yr, Yw
 
 
@@ -190,6 +198,13 @@ def group_op(op: str, X, G, ngroups: int, method="average", present=None):
     _check_present(present, D, A)
     if G.dtype != torch.int32 or tuple(G.shape) != (D, A):
         raise _lib.FmxError("G must be int32 [D][A]")
+    if op == "rank" and A > 4096 and ngroups > 0:
+        ok = G >= 0 if present is None else (G >= 0) & (present != 0)
+        cnt = torch.zeros((D, ngroups), dtype=torch.int32, device=G.device)
+        cnt.scatter_add_(1, G.clamp_min(0).long(), ok.int())
+        if int(cnt.max()) > 8192:
+            raise _lib.FmxError("group_rank_normalized on rows > 4096 assets sorts each group in LDS: "
+                                "at most 8192 members per (date, group)")
     Y = torch.empty_like(X)
     call("fmx_group_op", GROUP[op], ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method], ptr(present),
          stream_ptr())
@@ -222,8 +237,10 @@ def bucket_codes(X, edges: np.ndarray):
 
 
 # ----------------------------------------------------------------------------- IC / selection
-def ic_daily(X, R, lags=(1,)):
-    """[n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta) for pairs (X[f][t-L], R[t])."""
+def ic_daily(X, R, lags=(1,), rank2=None):
+    """[n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta) for pairs (X[f][t-L], R[t]).
+    ``rank2``: the doubled ranks of X from ``cs_rank_winsor(X, rank2=...)`` -- the rows
+    are then not ranked again (fmx_ic_daily_ranked, identical records)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
@@ -231,6 +248,12 @@ def ic_daily(X, R, lags=(1,)):
         raise _lib.FmxError("R must be a contiguous float64 [D][A] device tensor")
     lag_h = (ctypes.c_int32 * len(lags))(*[int(v) for v in lags])
     out = torch.empty((len(lags), 4, F, D), dtype=F64, device=X.device)
+    if rank2 is not None:
+        if rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+            raise _lib.FmxError("rank2 must be a contiguous int32 [F][D][A] tensor")
+        call("fmx_ic_daily_ranked", ptr(X), ptr(rank2), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p),
+             len(lags), ptr(out), stream_ptr())
+        return out
     call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p), len(lags), ptr(out),
          stream_ptr())
     return out
@@ -334,6 +357,24 @@ def corr_matrix(X, d0=0, d1=None, stats=None):
     else:
         G, N = gram_chunked(X, d0, d1)
     return torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
+
+
+def corr_prune_windows(X, stats, metrics, order, window: int, s0, use_rank_icir=True, threshold=-np.inf, rho=0.7,
+                       top_x=5):
+    """Rolling corr_prune selection on the device (fmx_corr_prune_windows): weights [J][F]."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    J = metrics.shape[0]
+    if tuple(metrics.shape) != (J, F, 8) or tuple(order.shape) != (J, F) or order.dtype != torch.int32:
+        raise _lib.FmxError("corr_prune_windows: metrics [J][F][8] and int32 order [J][F] expected")
+    s0h = (ctypes.c_int32 * J)(*[int(v) for v in s0])
+    w = torch.empty((J, F), dtype=F64, device=X.device)
+    top = F if top_x is None else int(top_x)
+    call("fmx_corr_prune_windows", ptr(X), ptr(stats.contiguous()), F, D, A, A, J, int(window),
+         ctypes.cast(s0h, ctypes.c_void_p), ptr(order.contiguous()), ptr(metrics.contiguous()), int(bool(use_rank_icir)),
+         float(threshold), float(rho), top, ptr(w), stream_ptr())
+    return w
 
 
 def greedy_prune(C, order, rho=0.7, top_x=None):

@@ -116,6 +116,10 @@ class FactorSelector:
         self._factors_lag = value
 
     # ------------------------------------------------------------------------------
+    def _contiguous(self, P):
+        dpos = P.dates.get_indexer(pd.Index(self.dates))
+        return len(dpos) == P.D and bool(np.all(dpos == np.arange(P.D)))
+
     def _window_metrics(self, P, X, R, proc_idx):
         """[J][F][8] metrics of each processed day's window (device)."""
         W = self.window
@@ -159,9 +163,21 @@ class FactorSelector:
         proc_idx = list(range(self.window, len(self.dates) - 1))
         M = self._window_metrics(P, X, R, proc_idx)                     # [J][F][8] on device
         kw = self.method_kwargs
-        if selector_func is icir_top_selector:
-            _, w = engine.select_icir_top(M, kw.get("use_rank_icir", True), kw.get("icir_threshold", 0.03),
-                                          kw.get("top_x", 5))
+        device_prune = (selector_func is corr_prune_selector and P.dense and len(names) <= engine.FUSED_GRAM_MAX_F
+                        and self._contiguous(P))
+        if selector_func is icir_top_selector or device_prune:
+            if selector_func is icir_top_selector:
+                _, w = engine.select_icir_top(M, kw.get("use_rank_icir", True), kw.get("icir_threshold", 0.03),
+                                              kw.get("top_x", 5))
+            else:
+                # the corr_prune plugin for every day at once: per-date Gram partials of the
+                # lag-1 factors pooled per window and the greedy walk on the device
+                order, _ = engine.select_icir_top(M, True, -np.inf, len(names))
+                _, stats = engine.cs_moment_stats("stats", X)
+                s0 = [i - self.window - 1 for i in proc_idx]
+                w = engine.corr_prune_windows(X, stats, M, order, self.window, s0, kw.get("use_rank_icir", True),
+                                              kw.get("icir_threshold", -np.inf), kw.get("rho", 0.7),
+                                              kw.get("top_x", 5))
             first = _metrics_frame(M[0].cpu().numpy(), names)
             cols = list(first.index)
             pos = [names.index(c) for c in cols]

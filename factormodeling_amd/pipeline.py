@@ -5,7 +5,8 @@ Step = the C2 hot path of BASELINE.json on a panel already resident in HBM:
      ts_decay(20), cs_rank, cs_zscore, cs_winsor, market_neutralize
      (operations.py; each writes its own output panel)
   2. daily IC / rank-IC / beta at lag 1 (single_factor_metrics) and lag 2
-     (FactorSelector windows) -- one fmx_ic_daily launch
+     (FactorSelector windows) -- one launch; when the operator set ranks X (cs_rank), the
+     IC starts from those ranks (fmx_ic_daily_ranked) instead of ranking X again
   3. full-sample metrics + rolling W-window metrics for every processed day
   4. icir_top selection per day (top_x=5, threshold=-1, factor_selector.py:94-139)
   5. correlation-based pruning: fp64-MFMA factor Gram + greedy prune (builder-defined)
@@ -222,8 +223,11 @@ class EngineBackend:
         return stats
 
     @staticmethod
-    def cs_rank_winsor(X, outs):
-        E.cs_rank_winsor(X, 0.01, 0.99, outs[0], outs[1])
+    def cs_rank_winsor(X, outs, rank2=None):
+        """``rank2``: also the doubled ranks the daily IC starts from."""
+        E.cs_rank_winsor(X, 0.01, 0.99, outs[0], outs[1], rank2=rank2)
+
+    ranked_ic_max_a = E.RANKED_IC_MAX_A
 
     def op(self, kind, op, w, X, out):
         if kind == "ts":
@@ -271,7 +275,8 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     ``plan_ops``; every operator writes its own output buffer (``bufs``: a list of tensors
     shaped like X, reused across steps; as many as the widest fused launch).  ``collect``
     (a dict) receives a copy of every operator's owned-date output (tests only); ``side``
-    (a dict) receives by-products later stages reuse (cs_zscore's row stats)."""
+    (a dict) receives by-products later stages reuse (cs_zscore's row stats; "rank2", the
+    doubled ranks of X, written into side["rank2_buf"] when it fits)."""
     stages = plan_ops(cfg.ops, be, cfg.fuse)
     need = max(len(o) for _, o in stages)
     bufs = list(bufs or [])
@@ -287,7 +292,15 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
             if side is not None:
                 side["stats"] = st
         elif name == "cs_rank_winsor":
-            be.cs_rank_winsor(X, outs)
+            if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
+                # the ranks of X also feed the daily IC (no second ranking of the panel)
+                rk = side.get("rank2_buf")
+                if rk is None or tuple(rk.shape) != tuple(X.shape):
+                    rk = torch.empty(X.shape, dtype=torch.int32, device=X.device)
+                side["rank2"] = rk
+                be.cs_rank_winsor(X, outs, rank2=rk)
+            else:
+                be.cs_rank_winsor(X, outs)
         else:
             kind, op, w = ops[0]
             if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
@@ -350,7 +363,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     t0 = _ev(timers)
     sp.exchange_halo()
     _rec(timers, "halo", t0)
-    side = {}
+    side = {"rank2_buf": getattr(sp, "rank2", None)}   # filled as "rank2" when this step ranks X
     if cfg.ops:
         sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
                           own=slice(sp.halo, None), side=side)
@@ -359,7 +372,11 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     # daily IC for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     lags = tuple(cfg.ic_lags)
-    daily = be.ic_daily(sp.X, sp.R, lags)[:, :, :, sp.halo:]          # [L][4][F][own]
+    if side.get("rank2") is not None:
+        sp.rank2 = side["rank2"]                                        # buffer reused next step
+        daily = be.ic_daily(sp.X, sp.R, lags, rank2=sp.rank2)[:, :, :, sp.halo:]
+    else:
+        daily = be.ic_daily(sp.X, sp.R, lags)[:, :, :, sp.halo:]      # [L][4][F][own]
     _rec(timers, "ic_daily", t0)
     t0 = _ev(timers)
     L = len(lags)

@@ -303,3 +303,41 @@ def test_c5_step_vs_oracle(dev):
     ref = OC.weighted_composite_factor(X, PL.factor_names(F), list(range(20, D - 1)), W, "zscore")
     assert_close(col["comp"].cpu().numpy().ravel(), ref.ravel(), rtol=RTOL, atol=ATOL, what="c5 composite")
     assert kept is None
+
+
+@pytest.mark.parametrize("A", [700, 5000, 10000])
+def test_group_ops_long_rows_vs_oracle(dev, A):
+    """Group ops at realistic row lengths (operations.py:112-168): the
+    per-group compaction / per-group sort kernels for A > 4096, bit-exact vs the oracle;
+    every rank method incl. 'dense'."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.ops as O
+    rng = np.random.default_rng(A)
+    D = 3
+    x = rng.standard_normal((D, A))
+    x = np.where(rng.random(x.shape) < 0.2, np.round(x, 1), x)
+    x[rng.random(x.shape) < 0.03] = np.nan
+    g = rng.integers(0, 11, size=(D, A)).astype(np.float64)
+    g[rng.random(g.shape) < 0.01] = np.nan                 # NaN group -> dropped
+    big = min(A, 8000)                                     # rank sorts a group in LDS: <= 8192
+    g[1, :big] = np.where(np.isnan(g[1, :big]), np.nan, 3.0)   # one big group on date 1
+    x[2, g[2] == 5] = 0.25                                 # a constant group (sd 0)
+    codes = np.where(np.isnan(g), -1, g).astype(np.int32)
+    Xd = torch.as_tensor(x[None], device=dev)
+    Gd = torch.as_tensor(codes, device=dev)
+    for op, fn in (("mean", O.group_mean), ("neutralize", O.group_neutralize), ("normalize", O.group_normalize)):
+        got = E.group_op(op, Xd, Gd, 11).cpu().numpy()[0]
+        with np.errstate(all="ignore"):
+            ref = fn(x, g)
+        assert_close(got.ravel(), ref.ravel(), exact=True, what=f"{op} A={A}")
+    for meth in ("average", "min", "max", "first", "dense"):
+        got = E.group_op("rank", Xd, Gd, 11, meth).cpu().numpy()[0]
+        ref = O.group_rank_normalized(x, g, method=meth)
+        assert_close(got.ravel(), ref.ravel(), exact=True, what=f"rank {meth} A={A}")
+    if A > 8192:                                           # a larger group fails loudly
+        from factormodeling_amd._lib import FmxError
+        G1 = Gd.clone()
+        G1[0] = 3
+        with pytest.raises(FmxError):
+            E.group_op("rank", Xd, G1, 11)

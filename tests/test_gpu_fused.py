@@ -110,3 +110,90 @@ def test_plan_ops_groups_the_c2_set():
     assert [s for s, _ in stages] == ["ts_set:20:10", "cs_zscore_neutralize", "cs_rank_winsor"]
     assert sorted(o for _, ops in stages for o in ops) == sorted(PL.OPS)
     assert len(PL.plan_ops(PL.OPS, PL.ENGINE, False)) == len(PL.OPS)
+
+
+def _ic_case(seed, F, D, A, r_nan, x_nan=0.02):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((F, D, A))
+    X = np.where(rng.random(X.shape) < 0.1, np.round(X, 1), X)      # ties
+    X[rng.random(X.shape) < x_nan] = np.nan
+    R = 0.01 * rng.standard_normal((D, A))
+    R[rng.random(R.shape) < r_nan] = np.nan
+    R[-1] = np.nan                             # forward returns not yet known
+    if D > 6:
+        R[3, : A // 2] = np.nan                # a long E list (tile path)
+        R[5, 2:] = np.nan                      # two pairs left
+        X[0, 4] = 0.25                         # constant exposures
+    return X, R
+
+
+@pytest.mark.parametrize("A,r_nan", [(9, 0.1), (300, 0.005), (1000, 0.05), (5000, 0.005), (5000, 0.03),
+                                     (10000, 0.005), (16384, 0.002)])
+@pytest.mark.parametrize("lags", [(1, 2), (1,), (0, 2, 5)])
+def test_ic_ranked_bit_identical(dev, A, r_nan, lags):
+    """Daily IC from cs_rank_winsor's doubled ranks == the standalone fused IC, record for
+    record (same element order and reductions), across short / long NaN-return lists."""
+    import torch
+    import factormodeling_amd.engine as E
+    F, D = (3, 9) if A <= 5000 else (2, 8)
+    X, R = _ic_case(A + len(lags), F, D, A, r_nan)
+    Xt, Rt = torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev)
+    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
+    got = E.ic_daily(Xt, Rt, lags, rank2=rk).cpu().numpy()
+    ref = E.ic_daily(Xt, Rt, lags).cpu().numpy()
+    assert np.array_equal(got, ref, equal_nan=True)
+
+
+def test_rank2_is_doubled_average_rank(dev):
+    import torch
+    from scipy.stats import rankdata
+    import factormodeling_amd.engine as E
+    X, _ = _ic_case(4, 2, 6, 777, 0.0, x_nan=0.05)
+    X[1, 2] = np.nan
+    X[1, 3, 1:] = np.nan                       # single valid value
+    Xt = torch.as_tensor(X, device=dev)
+    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
+    got = rk.cpu().numpy()
+    for f in range(2):
+        for d in range(6):
+            x = X[f, d]
+            ok = ~np.isnan(x)
+            exp = np.zeros(x.shape, dtype=np.int64)
+            if ok.any():
+                exp[ok] = (2 * rankdata(x[ok], method="average")).astype(np.int64)
+            assert np.array_equal(got[f, d].astype(np.int64), exp), (f, d)
+
+
+def test_rank2_rejects_presence_mask(dev):
+    import torch
+    import factormodeling_amd.engine as E
+    from factormodeling_amd._lib import FmxError
+    X = torch.zeros((1, 3, 10), dtype=torch.float64, device=dev)
+    pres = torch.ones((3, 10), dtype=torch.uint8, device=dev)
+    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    with pytest.raises(FmxError):
+        E.cs_rank_winsor(X, 0.01, 0.99, present=pres, rank2=rk)
+
+
+def test_step_ranked_ic_matches_unranked(dev):
+    """The C2 step's IC stage through the operator set's ranks gives the same daily
+    records, selection and pruning as the standalone IC."""
+    import torch
+    from factormodeling_amd import pipeline as PL
+
+    class Unranked(PL.EngineBackend):
+        ranked_ic_max_a = 0
+
+    cfg = PL.StepConfig(sel_window=10)
+    out = []
+    for be in (PL.ENGINE, Unranked()):
+        sp = PL.ShardedPanel(60, 400, 6, 0, 1, dev, seed=3, halo=cfg.halo)
+        col = {}
+        w, kept = PL.run_step(sp, cfg, be=be, collect=col)
+        out.append((col["daily"].cpu().numpy(), w.cpu().numpy(), kept, getattr(sp, "rank2", None) is not None))
+    assert out[0][3] and not out[1][3]
+    assert np.array_equal(out[0][0], out[1][0], equal_nan=True)
+    assert np.array_equal(out[0][1], out[1][1])
+    assert list(out[0][2]) == list(out[1][2])
