@@ -39,7 +39,8 @@ SIGNATURES = {
     "fmx_elementwise": [c_i32, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_vp],
     "fmx_bucket": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "fmx_ic_daily": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
-    "fmx_ic_daily_ranked": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "fmx_ic_ranked_work_len": [c_i64, c_i64],
+    "fmx_ic_daily_ranked": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp],
     "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
@@ -63,7 +64,7 @@ SIGNATURES = {
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"fmx_last_error": c_cp}
+_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)

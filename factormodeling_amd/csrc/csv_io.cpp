@@ -341,6 +341,11 @@ void parse_chunk(Chunk& c, int ncol, int dcol, int scol, int F) {
       c.err = "data row " + std::to_string(c.rows) + ": date '" + std::string(f[dcol]) + "' is not ISO YYYY-MM-DD[ HH:MM[:SS[.f]]]";
       return;
     }
+    if (scol >= 0 && is_na(f[scol])) {   // pandas would read a NaN symbol ('NA' is a ticker)
+      c.err = "data row " + std::to_string(c.rows) + ": symbol '" + std::string(f[scol]) +
+              "' is one of pandas' NA spellings (pandas reads it as NaN): not supported";
+      return;
+    }
     c.date_ns.push_back(ns);
     c.sym.push_back(scol >= 0 ? f[scol] : std::string_view());
     int v = 0;
@@ -548,6 +553,11 @@ int fmx_csv_open(const char* path, const char* date_col, const char* symbol_col,
       delete h;
       return fail(FMX_IO_ERR_FORMAT, "quoted header fields are not supported");
     }
+    for (int i = 0; i < j; ++i)
+      if (cols[i] == cols[j]) {   // pandas renames the second to 'x.1': not mirrored
+        delete h;
+        return fail(FMX_IO_ERR_FORMAT, "duplicate header name '" + cols[j] + "' is not supported");
+      }
     if (cols[j] == date_col && dcol < 0) dcol = j;
     else if (has_sym && cols[j] == symbol_col && scol < 0) scol = j;
   }

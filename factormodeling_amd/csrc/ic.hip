@@ -298,11 +298,17 @@ extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, 
   FMX_ARG(n_lags >= 1 && n_lags <= 8, "n_lags");
   for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
   if (F == 0 || D == 0) return FMX_OK;
-  if (A <= 16384) return br_ic_daily(X, R, F, D, A, ld, lags, n_lags, out, as_stream(stream));
+  if (A <= 16384) {
+    const fmx_status e = br_ic_daily(X, R, F, D, A, ld, lags, n_lags, out, as_stream(stream));
+    if (e != FMX_ERR_UNSUPPORTED) return e;
+  }
   // very wide rows: one LDS-bitonic workgroup per (factor, date, lag)
   int P = next_pow2((int)std::max<int64_t>(A, 2));
   size_t lds = (size_t)P * 10 + 16 + 16 * 8 + 16 * 4 + 64;
-  if (lds > 160 * 1024) { set_error("A too large for the IC kernels"); return FMX_ERR_UNSUPPORTED; }
+  if (lds > 160 * 1024) {
+    set_error("A too large for the IC kernels' LDS (A <= 12288; longer rows: fmx_ic_daily_ranked)");
+    return FMX_ERR_UNSUPPORTED;
+  }
   int32_t* lags_dev = nullptr;
   hipStream_t st = as_stream(stream);
   FMX_HIP(hipMallocAsync((void**)&lags_dev, sizeof(int32_t) * n_lags, st));
@@ -318,15 +324,18 @@ extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, 
   return FMX_OK;
 }
 
+extern "C" int64_t fmx_ic_ranked_work_len(int64_t F, int64_t D) { return ic_ranked_work_len(F, D); }
+
 extern "C" fmx_status fmx_ic_daily_ranked(const double* X, const uint32_t* rank2, const double* R, int64_t F,
                                           int64_t D, int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags,
-                                          double* out, void* stream) {
-  FMX_ARG(X && rank2 && R && out && lags, "null pointer");
+                                          int32_t* work, int64_t work_len, double* out, void* stream) {
+  FMX_ARG(X && rank2 && R && out && lags && work, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
   FMX_ARG(n_lags >= 1 && n_lags <= 8, "n_lags");
+  FMX_ARG(work_len >= ic_ranked_work_len(F, D), "work shorter than fmx_ic_ranked_work_len(F, D)");
   for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
   if (F == 0 || D == 0) return FMX_OK;
-  return br_ic_ranked(X, rank2, R, F, D, A, ld, lags, n_lags, out, as_stream(stream));
+  return br_ic_ranked(X, rank2, R, F, D, A, ld, lags, n_lags, out, work, as_stream(stream));
 }
 
 extern "C" fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev,

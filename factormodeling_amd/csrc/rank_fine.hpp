@@ -46,7 +46,7 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 //
 // RK (optional): 2 * average rank among the row's valid keys, i.e. 2*#less + #equal + 1
 // (0 for NaN / absent), as uint32 -- the daily IC of the same rows starts from it
-// (k_ic_ranked) instead of ranking them again.
+// (k_ic_wave) instead of ranking them again.
 template <int NT, int EMAX, bool PRES, bool WQ = false>
 __global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
@@ -716,16 +716,19 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
 // Daily IC from the ranks the cs_rank pass of the same panel already produced (RK =
 // 2*#less + #equal + 1 among the row's non-NaN exposures, k_cs_rank_fa), so no sort or
 // histogram is repeated.  The pairs of lag m are the non-NaN exposures minus E_m, those
-// whose lag-m return is NaN; the doubled pair rank is RK - (2*#less + #equal) over E_m.
-// E_m holds the row's NaN returns -- a few keys: gathered in LDS while the row loads,
-// sorted by one wave when <= 64 and binary-searched (#less + #less-or-equal is exactly
-// the correction); a longer E_m is gathered register-chunk by chunk and scanned.
-// Sums, moments and their reductions repeat k_ic_daily_fr step for step (same element
-// order, same butterflies), so the records are bit-identical to it.
+// whose lag-m return is NaN; the doubled pair rank is RK - (2*#less + #equal) over E_m
+// (#less + #less-or-equal: exactly the correction).
+//
+// ic_ranked_row: one 1024-thread workgroup per row, any E_m -- the rows the wave kernel
+// (k_ic_wave, below) hands over.  E_m keys gathered in LDS while the row loads, sorted by
+// one wave when < 64 (a sentinel ends the list) and binary-searched; a longer E_m is
+// gathered register-chunk by chunk and scanned.  Sums and two-pass moments as in
+// k_ic_daily_fr (same element order, same butterflies: the records are bit-identical).
 template <int NT, int EMAX>
-__global__ void __launch_bounds__(NT, (NT == 1024 && EMAX <= 5) ? 8 : 4)
-k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
-            int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out) {
+__device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restrict__ X,
+                                              const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
+                                              int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL,
+                                              double* __restrict__ out) {
   constexpr int NW = NT / 64, ES = 64;
   __shared__ double dscr[(NW + 1) * 16];
   __shared__ uint64_t el[2][ES];              // E_m keys (first ES), then sorted
@@ -733,7 +736,8 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
   __shared__ int ecnt[2], wcnt[NW];
   __shared__ double cst[8], fin[16];
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t s = blockIdx.x / F, f = blockIdx.x % F;
+  BR_PH_INIT;
+  const int64_t s = row / F, f = row % F;
   const double* xf = X + (f * D + s) * ld;
   const uint32_t* rkf = RK + (f * D + s) * ld;
   const int lagv[2] = {L0, L1};
@@ -790,6 +794,7 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
     cw0 += __popcll(__ballot(mm & 1));
     cw1 += __popcll(__ballot(mm & 2));
   }
+  BR_PH();
   fr_part_bfly<4, false>(v1, dscr, 16, 0);
   if ((t & 63) == 0) {
     dscr[wid * 16 + 4] = (double)cw0;
@@ -809,6 +814,7 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
   }
   const double n[2] = {tot[4], tot[5]};
   const bool need = (act[0] && n[0] >= 3.0) || (act[1] && n[1] >= 3.0);
+  BR_PH();
   if (need) {
     // doubled ranks (loads in flight over the E sort)
     uint32_t rk[EMAX];
@@ -816,11 +822,12 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
     for (int k = 0; k < EMAX; ++k) rk[k] = (k < EMAX - 1 || last_in) ? rkf[t + k * NT] : 0u;
     const int ne[2] = {__builtin_amdgcn_readfirstlane(ecnt[0]), __builtin_amdgcn_readfirstlane(ecnt[1])};
     const int nw = wid == 0 ? ne[0] : ne[1];
-    if (wid < 2 && nw > 0 && nw <= ES) {
+    if (wid < 2 && nw > 0 && nw < ES) {
       const uint64_t v = lane < nw ? el[wid][lane] : KEY_SENTINEL;
       el[wid][lane] = wave_sort64(v, lane);
     }
     __syncthreads();
+    BR_PH();
     // cr[k] = doubled pair rank of lag 0 | lag 1 << 16: RK minus the E corrections (every
     // partial difference stays >= the final one >= 2, so the fields never borrow)
     uint32_t cr[EMAX];
@@ -831,7 +838,7 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
       const uint64_t key = okey(xv[k]);
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        if (!((pm >> (2 * k + m)) & 1) || ne[m] == 0 || ne[m] > ES) continue;
+        if (!((pm >> (2 * k + m)) & 1) || ne[m] == 0 || ne[m] >= ES) continue;
         int lo = 0, le = 0;
 #pragma unroll
         for (int st = ES / 2; st > 0; st >>= 1) {
@@ -843,7 +850,7 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      if (ne[m] <= ES) continue;
+      if (ne[m] < ES) continue;
       // long E_m: gather register chunk c's E members in asset order, scan them
 #pragma unroll 1
       for (int c = 0; c < EMAX; ++c) {
@@ -878,6 +885,7 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
         }
       }
     }
+    BR_PH();
     double fm[2], rm[2], km[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -904,11 +912,27 @@ k_ic_ranked(const double* __restrict__ X, const uint32_t* __restrict__ RK, const
       }
       fr_part_bfly<8, false>(w, dscr, 16, 8 * m);
     }
+    BR_PH();
     fr_fin_dpp<NT>(dscr, 16, 16);
     if (t < 16) fin[t] = dscr[NW * 16 + t];
     __syncthreads();
   }
   if (t == 0) fr_ic_store(out, F, D, s, f, lagv, act, n, cst, fin);
+  BR_PH();
+}
+
+// The rows listed by k_ic_wave (list[0] = count, then row ids): a grid of workgroups
+// walks the list.
+template <int NT, int EMAX>
+__global__ void __launch_bounds__(NT, 4)
+k_ic_ranked_list(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
+                 int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
+                 const int32_t* __restrict__ list) {
+  const int n = list[0];
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    ic_ranked_row<NT, EMAX>(list[1 + i], X, RK, Rt, F, D, A, ld, L0, L1, NL, out);
+    __syncthreads();                          // LDS reused by the next row
+  }
 }
 
 }  // namespace fmx

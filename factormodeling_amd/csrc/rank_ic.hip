@@ -29,6 +29,11 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
   auto fr_table = FMX_EMAX_TABLE(k_ic_daily_fr);
   const bool fine = rank_impl() == RANK_IMPL_FINE && lds_fits(fr_table(nt, br_emax(A, nt)), lds_fr);
   const size_t lds = fine ? lds_fr : (size_t)std::max<int64_t>(A, nt) * 8 + (size_t)((A + 15) & ~15ll);
+  if (!fine && !lds_fits(FMX_EMAX_TABLE(k_ic_daily_br)(nt, br_emax(A, nt)), lds)) {
+    set_error("row too long for the IC kernels' LDS (rank it once with fmx_cs_rank_winsor and use "
+              "fmx_ic_daily_ranked)");
+    return FMX_ERR_UNSUPPORTED;
+  }
   for (int base = 0; base < n_lags; base += 2) {
     int NL = std::min(2, n_lags - base);
     int L0 = lags_host[base], L1 = NL > 1 ? lags_host[base + 1] : 0;
@@ -44,21 +49,262 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
   return FMX_OK;
 }
 
-// Daily IC from the doubled ranks of the same panel (k_ic_ranked): A <= 16384.
+// ------------------------------------------------------------------------------------
+// NaN-return positions per date (the candidates of every row's E lists): one wave per
+// date, ballot-compacted in asset order; npos[t] = the full count, pos[t][0..ICW_PC) the
+// first ICW_PC positions.
+constexpr int ICW_PC = 256;
+__global__ void __launch_bounds__(256)
+k_nan_positions(const double* __restrict__ Rt, int64_t D, int64_t A, int64_t ld, int32_t* __restrict__ pos,
+                int32_t* __restrict__ npos) {
+  const int lane = threadIdx.x & 63;
+  const int64_t d = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= D) return;
+  const double* r = Rt + d * ld;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int c = 0;
+  for (int64_t i0 = 0; i0 < A; i0 += 64) {
+    const int64_t i = i0 + lane;
+    const bool nan = i < A && !(r[i] == r[i]);
+    const uint64_t b = __ballot(nan);
+    const int at = c + __popcll(b & lt);
+    if (nan && at < ICW_PC) pos[d * ICW_PC + at] = (int32_t)i;
+    c += __popcll(b);
+  }
+  if (lane == 0) npos[d] = c;
+}
+
+// ------------------------------------------------------------------------------------
+// Daily IC from the ranks, one WAVE per row: no workgroup barrier anywhere, so ~20 rows
+// are in flight per CU instead of two 1024-thread rows.
+//  1. E_m from the target date's NaN-return positions: gather x there (< 64 valid, else
+//     the row goes to the overflow list for ic_ranked_row), wave-sort in LDS.
+//  2. one streaming pass over x, RK and the two return rows: per lag, the pair count
+//     (ballots) and sums shifted by the lag's first pair (single-pass moments without
+//     cancellation; constant inputs = nothing differs from that pair); the pair rank is
+//     RK minus a binary search over sorted E_m.
+//  3. multi-value DPP butterflies, lane 0 writes the records.
+// Moments are single-pass about the first pair (rank moments from exact integer sums), so
+// records agree with the two-pass kernels to ~1e-15 relative, not bitwise.
+constexpr int ICW_WAVES = 4;
+#ifndef ICW_UNROLL
+#define ICW_UNROLL 1
+#endif
+__device__ __forceinline__ int icw_search(const uint64_t* e, uint64_t key) {
+  // #keys < key plus #keys <= key in the sorted, sentinel-terminated list of < 64 keys
+  int lo = 0, le = 0;
+#pragma unroll
+  for (int st = 32; st > 0; st >>= 1) {
+    lo += e[lo + st - 1] < key ? st : 0;
+    le += e[le + st - 1] <= key ? st : 0;
+  }
+  return lo + le;
+}
+
+#ifndef ICW_MINW
+#define ICW_MINW 6
+#endif
+__global__ void __launch_bounds__(64 * ICW_WAVES, ICW_MINW)
+k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt, int64_t F,
+          int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
+          const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
+  __shared__ uint64_t el[ICW_WAVES][2][64];
+  __shared__ double scr[ICW_WAVES * 32];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * ICW_WAVES + wid;
+  if (row >= F * D) return;                   // whole waves; no workgroup barrier below
+  const int64_t s = row / F, f = row % F;
+  const int lagv[2] = {L0, L1};
+  const double* rr[2];
+  bool act[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    act[m] = m < NL && s + lagv[m] < D;
+    rr[m] = Rt + (act[m] ? s + lagv[m] : s) * ld;
+  }
+  if (!act[0] && !act[1]) return;
+  const double* xf = X + (f * D + s) * ld;
+  const uint32_t* rkf = RK + (f * D + s) * ld;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // 1. E lists
+  int ne[2] = {0, 0};
+  bool over = false;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    if (!act[m]) continue;
+    const int64_t td = s + lagv[m];
+    const int c = npos[td];
+    if (c > ICW_PC) { over = true; continue; }
+    int k = 0;
+    for (int b = 0; b < c; b += 64) {
+      const int j = b + lane;
+      double v = qnan();
+      if (j < c) v = xf[pos[td * ICW_PC + j]];
+      const bool e = v == v;
+      const uint64_t bal = __ballot(e);
+      const int at = k + __popcll(bal & lt);
+      if (e && at < 64) el[wid][m][at] = okey(v);
+      k += __popcll(bal);
+    }
+    if (k >= 64) over = true;
+    ne[m] = k;
+  }
+  if (over) {                                 // a long E list: the workgroup kernel takes the row
+    if (lane == 0) {
+      const int q = atomicAdd(&ovf[0], 1);
+      ovf[1 + q] = (int32_t)row;
+    }
+    return;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    if (ne[m] == 0) continue;
+    const uint64_t v = lane < ne[m] ? el[wid][m][lane] : KEY_SENTINEL;
+    __builtin_amdgcn_wave_barrier();
+    el[wid][m][lane] = wave_sort64(v, lane);
+  }
+  // 2. one pass.  Per lag: pair count (ballots); the first pair's (x, r) is the lag's
+  // shift (a, b) and reference (constant inputs: no pair differs from it); sums of x', r',
+  // x'^2, r'^2, x'r' (x' = x - a, r' = r - b), of 2k * r' and (2k)^2 (exact integers) with
+  // 2k = RK minus the E correction.
+  double sm[2][6];
+  uint64_t kk[2] = {0, 0};
+  double ax[2] = {0.0, 0.0}, ar[2] = {0.0, 0.0};
+  bool ref[2] = {false, false};
+  int cnt[2] = {0, 0};
+  uint32_t dif = 0;                           // bit 2m: an x differs from lag m's reference, 2m+1: an r
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) sm[m][q] = 0.0;
+  const int An = (int)A;
+#pragma unroll ICW_UNROLL
+  for (int i0 = 0; i0 < An; i0 += 64) {
+    const int i = i0 + lane;
+    const bool in = i < An;
+    const double x = in ? xf[i] : qnan();
+    const uint32_t rk = in ? rkf[i] : 0u;
+    double r[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) r[m] = (in && act[m]) ? rr[m][i] : qnan();
+    const uint64_t key = okey(x);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const bool p = x == x && r[m] == r[m];
+      const uint64_t bp = __ballot(p);
+      if (!bp) continue;
+      cnt[m] += __popcll(bp);
+      if (!ref[m]) {                          // wave-uniform: the first chunk with pairs
+        const int l = __ffsll((unsigned long long)bp) - 1;
+        ax[m] = fr_readlane_d(x, l);
+        ar[m] = fr_readlane_d(r[m], l);
+        ref[m] = true;
+      }
+      if (!p) continue;
+      const int corr = ne[m] ? icw_search(el[wid][m], key) : 0;
+      const uint32_t k2 = rk - (uint32_t)corr;
+      const double dx = x - ax[m], dy = r[m] - ar[m];
+      dif |= ((x != ax[m]) ? 1u : 0u) << (2 * m);
+      dif |= ((r[m] != ar[m]) ? 1u : 0u) << (2 * m + 1);
+      sm[m][0] += dx; sm[m][1] += dy;
+      sm[m][2] += dx * dx; sm[m][3] += dy * dy; sm[m][4] += dx * dy;
+      sm[m][5] += (double)k2 * dy;
+      kk[m] += (uint64_t)k2 * k2;
+    }
+  }
+  // 3. butterflies into the wave's scratch: [0,6) lag 0's sums, [6,12) lag 1's, [12,14) the
+  // (2k)^2 sums (exact in doubles: < 2^53)
+  double* sc = scr + wid * 32;
+  {
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) { a[q] = sm[0][q]; a[6 + q] = sm[1][q]; }
+    a[12] = (double)kk[0];
+    a[13] = (double)kk[1];
+    a[14] = a[15] = 0.0;
+    fr_part_bfly<16, false>(a, scr, 32, 0);
+  }
+  uint32_t dflags = 0;                        // wave OR of the difference bits
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dflags |= (__ballot((dif >> q) & 1) != 0 ? 1u : 0u) << q;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if (!act[m]) continue;
+      const int64_t td = s + lagv[m];
+      double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
+      const int64_t stp = F * D;
+      const double nn = (double)cnt[m];
+      double ic = qnan(), ric = qnan(), beta = qnan();
+      if (cnt[m] >= 3) {
+        const double* w = sc + 6 * m;
+        const double sx = w[0], sy = w[1];
+        const bool fconst = !((dflags >> (2 * m)) & 1), rconst = !((dflags >> (2 * m + 1)) & 1);
+        if (!fconst && !rconst) {
+          const double sxy = w[4] - sx * sy / nn;
+          const double sxx = w[2] - sx * sx / nn;
+          const double syy = w[3] - sy * sy / nn;
+          // ranks: sum k = n(n+1)/2 (ties keep it), sum k^2 = sum (2k)^2 / 4: both exact
+          const double skk = sc[12 + m] / 4.0 - nn * (nn + 1.0) * (nn + 1.0) / 4.0;
+          const double sky = 0.5 * w[5] - 0.5 * (nn + 1.0) * sy;
+          ic = fmin(1.0, fmax(-1.0, sxy / sqrt(sxx * syy)));
+          ric = fmin(1.0, fmax(-1.0, sky / sqrt(skk * syy)));
+        }
+        // beta = sum x r / sum x^2 from the shifted sums
+        const double a = ax[m], b = ar[m];
+        const double sxx_raw = w[2] + 2.0 * a * sx + nn * a * a;
+        const double sxr_raw = w[4] + a * sy + b * sx + nn * a * b;
+        beta = sxx_raw > 0 ? sxr_raw / sxx_raw : qnan();
+      }
+      o[0] = nn;
+      o[stp] = ic;
+      o[2 * stp] = ric;
+      o[3 * stp] = beta;
+    }
+  }
+}
+
+
+// Daily IC from the doubled ranks of the same panel: k_nan_positions, then k_ic_wave (one
+// wave per row), then k_ic_ranked_list over the rows whose E lists were too long.
+// work: [D][ICW_PC] positions, [D] counts, [1 + F*D] overflow list.  A <= 16384.
+int64_t ic_ranked_work_len(int64_t F, int64_t D) { return D * (ICW_PC + 1) + 1 + F * D; }
+
 fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
-                        int64_t ld, const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
+                        int64_t ld, const int32_t* lags_host, int n_lags, double* out, int32_t* work, hipStream_t st) {
   const int nt = 1024;
-  if (br_emax(A, nt) < 0) { set_error("row too long for the ranked IC kernel (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
+  const void* kl = FMX_EMAX_TABLE(k_ic_ranked_list)(nt, br_emax(A, nt));
+  if (!kl) { set_error("row too long for the ranked IC kernels (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  int32_t* pos = work;
+  int32_t* npos = work + D * ICW_PC;
+  int32_t* ovf = npos + D;
+  k_nan_positions<<<(unsigned)((D + 3) / 4), 256, 0, st>>>(R, D, A, ld, pos, npos);
+  FMX_LAUNCH_CHECK("k_nan_positions");
+  static const int list_grid = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return 2 * std::max(cus, 1);              // two 1024-thread rows per CU
+  }();
+  const unsigned wave_grid = (unsigned)((F * D + ICW_WAVES - 1) / ICW_WAVES);
   for (int base = 0; base < n_lags; base += 2) {
     int NL = std::min(2, n_lags - base);
     int L0 = lags_host[base], L1 = NL > 1 ? lags_host[base + 1] : 0;
     double* o = out + (int64_t)base * 4 * F * D;
     k_ic_empty<<<(unsigned)F, 64, 0, st>>>(o, F, D, L0, L1, NL);
     FMX_LAUNCH_CHECK("k_ic_empty");
+    FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
+    k_ic_wave<<<wave_grid, 64 * ICW_WAVES, 0, st>>>(X, RK, R, F, D, A, ld, L0, L1, NL, o, pos, npos, ovf);
+    FMX_LAUNCH_CHECK("k_ic_wave");
     void* args[] = {(void*)&X, (void*)&RK, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,
-                    (void*)&L1, (void*)&NL, (void*)&o};
-    fmx_status e = launch_br(FMX_EMAX_TABLE(k_ic_ranked), nt, A, F * D, 0, args, st);
-    if (e) return e;
+                    (void*)&L1, (void*)&NL, (void*)&o, (void*)&ovf};
+    const unsigned g = (unsigned)std::min<int64_t>(F * D, list_grid);
+    FMX_HIP(hipLaunchKernel(kl, dim3(g), dim3(nt), args, 0, st));
   }
   return FMX_OK;
 }

@@ -330,6 +330,7 @@ fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                        const int32_t* lags_host, int n_lags, double* out, hipStream_t st);
 fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
-                        int64_t ld, const int32_t* lags_host, int n_lags, double* out, hipStream_t st);
+                        int64_t ld, const int32_t* lags_host, int n_lags, double* out, int32_t* work, hipStream_t st);
+int64_t ic_ranked_work_len(int64_t F, int64_t D);
 
 }  // namespace fmx

@@ -30,7 +30,8 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   __shared__ int s_npos, s_nneg, s_npres;
   __shared__ unsigned s_hist[512];
   __shared__ uint64_t s_prefix[2], s_mask[2];
-  __shared__ unsigned s_krem[2];
+  __shared__ unsigned s_krem[2], s_tie[2];
+  __shared__ unsigned s_wt[2][SIM_BLOCK / 64];
   const int64_t d = blockIdx.x, mgr = blockIdx.y;   // managers batched along y
   X += mgr * D * A;
   W += mgr * D * A;
@@ -68,6 +69,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
     s_mask[0] = s_mask[1] = 0;
     s_krem[0] = (unsigned)nl;
     s_krem[1] = (unsigned)ns;
+    s_tie[0] = s_tie[1] = 0;
   }
   __syncthreads();
   // k-th extreme of each leg by an 8-pass radix select over the 64-bit keys (positive
@@ -114,6 +116,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
             cum += cs[j];
           }
           bin -= j;
+          if (pass == 7) s_tie[leg] = cs[j];   // #keys equal to the k-th key
           s_krem[leg] = need - cum;
           s_prefix[leg] |= (uint64_t)bin << shift;
           s_mask[leg] |= (uint64_t)255 << shift;
@@ -124,21 +127,47 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   }
   const uint64_t t0 = s_prefix[0], t1 = s_prefix[1];
   const unsigned r0 = s_krem[0], r1 = s_krem[1];
-  for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
-    const double v = sx[a];
+  // Exact ties at a leg's k-th key go to the lowest asset indices: when a leg has more
+  // keys equal to its k-th than it still needs, each tied element's index among them comes
+  // from a block-wide scan (wave ballots + per-wave totals), chunk by chunk in asset order.
+  const bool scan = !flat && (s_tie[0] > r0 || s_tie[1] > r1);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned base0 = 0, base1 = 0;                      // ties in earlier chunks
+  for (int64_t a0 = 0; a0 < A; a0 += SIM_BLOCK) {
+    const int64_t a = a0 + threadIdx.x;
+    const bool in = a < A;
+    const double v = in ? sx[a] : __builtin_nan("");
+    const bool lg = v > 0.0;
+    const uint64_t k = (uint64_t)__double_as_longlong(lg ? v : -v);
+    const bool tie0 = !flat && lg && k == t0, tie1 = !flat && v < 0.0 && k == t1;
+    unsigned before = 0;
+    if (scan) {
+      const uint64_t b0 = __ballot(tie0), b1 = __ballot(tie1);
+      const uint64_t lt = (1ull << lane) - 1ull;
+      if (lane == 0) { s_wt[0][wid] = __popcll(b0); s_wt[1][wid] = __popcll(b1); }
+      __syncthreads();
+      unsigned off0 = 0, off1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+      for (int q = 0; q < SIM_BLOCK / 64; ++q) {
+        const unsigned c0 = s_wt[0][q], c1 = s_wt[1][q];
+        off0 += q < wid ? c0 : 0u;
+        off1 += q < wid ? c1 : 0u;
+        tot0 += c0;
+        tot1 += c1;
+      }
+      __syncthreads();                                // s_wt reused by the next chunk
+      before = tie0 ? base0 + off0 + (unsigned)__popcll(b0 & lt) : base1 + off1 + (unsigned)__popcll(b1 & lt);
+      base0 += tot0;
+      base1 += tot1;
+    }
+    if (!in) continue;
     double out = 0.0;
     if ((p && !p[a]) || (nan_absent && v != v)) {
       out = __builtin_nan("");
     } else if (!flat && (v > 0.0 || v < 0.0)) {
-      const bool lg = v > 0.0;
-      const uint64_t k = (uint64_t)__double_as_longlong(lg ? v : -v);
       const uint64_t t = lg ? t0 : t1;
       bool sel = k > t;
-      if (k == t) {  // exact tie at the k-th key: lowest asset indices first
-        unsigned before = 0;
-        for (int64_t b = 0; b < a; ++b) before += (sx[b] == v);
-        sel = before < (lg ? r0 : r1);
-      }
+      if (k == t) sel = scan ? before < (lg ? r0 : r1) : true;
       if (sel) out = lg ? wl : wsh;
     }
     w[a] = out;

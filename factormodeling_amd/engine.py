@@ -149,6 +149,16 @@ def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=Fal
 
 
 RANKED_IC_MAX_A = 16384
+_WORK = {}
+
+
+def _workspace(device, n):
+    """Per-device int32 scratch reused across calls (grown on demand; ops on one stream)."""
+    w = _WORK.get(device)
+    if w is None or w.numel() < n:
+        w = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+        _WORK[device] = w
+    return w
 
 
 def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None, rank2=None):
@@ -251,8 +261,10 @@ def ic_daily(X, R, lags=(1,), rank2=None):
     if rank2 is not None:
         if rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
             raise _lib.FmxError("rank2 must be a contiguous int32 [F][D][A] tensor")
+        n = int(_lib.load().fmx_ic_ranked_work_len(F, D))
+        work = _workspace(X.device, n)
         call("fmx_ic_daily_ranked", ptr(X), ptr(rank2), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p),
-             len(lags), ptr(out), stream_ptr())
+             len(lags), ptr(work), n, ptr(out), stream_ptr())
         return out
     call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p), len(lags), ptr(out),
          stream_ptr())

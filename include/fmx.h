@@ -180,10 +180,13 @@ fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, 
                         const int32_t* lags, int32_t n_lags, double* out, void* stream);
 /* fmx_ic_daily for a panel whose rows fmx_cs_rank_winsor already ranked (rank2): the
  * rank among each lag's pairs is rank2 corrected by the exposures whose return is NaN, so
- * no row is ranked again.  Records bit-identical to fmx_ic_daily.  A <= 16384. */
+ * no row is ranked again; one wavefront per row (single-pass shifted moments: records
+ * agree with fmx_ic_daily to ~1e-15 relative, pair counts exactly).  work: device int32
+ * scratch of fmx_ic_ranked_work_len(F, D) elements.  A <= 16384. */
+int64_t fmx_ic_ranked_work_len(int64_t F, int64_t D);
 fmx_status fmx_ic_daily_ranked(const double* X, const uint32_t* rank2, const double* R, int64_t F, int64_t D,
-                               int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags, double* out,
-                               void* stream);
+                               int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags, int32_t* work,
+                               int64_t work_len, double* out, void* stream);
 /* Window summaries of one lag's daily stats [4][F][D] over J date windows [d0, d1).
  * out: [J][F][8] = IC, IC_IR, rank_IC, rank_IC_IR, tstat, n_beta, pct_pos, n_days. */
 fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev, const int32_t* d1_dev,

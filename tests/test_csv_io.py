@@ -154,6 +154,11 @@ def test_duplicates_and_unsorted_rows_flagged(tmp_path):
     ('date,symbol,x\n2015-01-01,"A",1\n', "quoted"),
     ("date,symbol,x\n01/02/2015,A,1\n", "ISO"),
     ("sym,x\nA,1\n", "lacks column"),
+    ("date,symbol,x\n2015-01-01,NA,1\n", "NA spellings"),     # pandas: NaN symbol
+    ("date,symbol,x\n2015-01-01,,1\n", "NA spellings"),
+    ("date,symbol,x\n2015-01-01,null,1\n", "NA spellings"),
+    ("date,symbol,x,x\n2015-01-01,A,1,2\n", "duplicate header"),  # pandas: 'x', 'x.1'
+    ("date,symbol,x\nNA,A,1\n", "ISO"),
 ])
 def test_format_errors_are_loud(tmp_path, text, msg):
     p = tmp_path / "e.csv"

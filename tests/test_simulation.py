@@ -79,6 +79,7 @@ def test_trade_equal_kernel_matches_oracle(D, A, pct, ragged):
     X[rng.random(X.shape) < 0.02] = 0.0
     X[2] = np.abs(X[2])  # flat day
     X[3, : A // 2] = np.round(X[3, : A // 2], 1)  # many exact ties, some at the k-th value
+    X[4] = rng.integers(-2, 3, A).astype(np.float64)  # discrete signal: a tie block of ~A/5 at the k-th
     present = rng.random((D, A)) >= 0.1 if ragged else np.ones((D, A), dtype=bool)
     dev = torch.device("cuda", 0)
     pres = torch.as_tensor(present.astype(np.uint8), device=dev) if ragged else None
