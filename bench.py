@@ -52,6 +52,8 @@ def bytes_per_unit(stage, F, ranked=False):
         return 24.0
     if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u32)
         return 28.0 if ranked else 24.0
+    if kind == "rank2":              # ranks-only pass: X once + the u32 doubled ranks
+        return 12.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
         return 16.0
     if kind == "ic_daily":              # X once (+ its u32 ranks when ranked) + two R rows
@@ -60,8 +62,8 @@ def bytes_per_unit(stage, F, ranked=False):
 
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
-STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_ranked<", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
-                "ts_set": "fmx::k_ts_set<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
+STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave(", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
+                "ts_set": ("fmx::k_ts_set2<", "fmx::k_ts_set<"), "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",

@@ -31,6 +31,7 @@ SIGNATURES = {
     "fmx_cs_moment_stats": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_zscore_neutralize": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_rank_winsor": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp, c_vp],
+    "fmx_cs_rank2": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
     "fmx_cs_filter_center": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
@@ -45,10 +46,13 @@ SIGNATURES = {
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_corr_prune_windows": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32,
-                               c_dbl, c_dbl, c_i32, c_vp, c_vp],
+                               c_dbl, c_dbl, c_i32, c_vp, c_vp, c_i64, c_vp],
+    "fmx_corr_prune_windows_work_bytes": [c_i64, c_i64, c_i64, c_i32, c_vp],
     "fmx_zscore_exposures_range": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
-    "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
-    "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp],
+    "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
+    "fmx_gram_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i32],
+    "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
+    "fmx_gram_fused_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
     "fmx_comp_adj": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
     "fmx_comp_proxy": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
@@ -64,7 +68,8 @@ SIGNATURES = {
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64}
+_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
+             "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)

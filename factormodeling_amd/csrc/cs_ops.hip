@@ -805,6 +805,14 @@ extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double*
   return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
 }
 
+extern "C" fmx_status fmx_cs_rank2(const double* X, uint32_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                   void* stream) {
+  FMX_ARG(X && rank2, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  return br_cs_rank2(X, rank2, F, D, A, ld, as_stream(stream));
+}
+
 extern "C" fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D, int64_t A,
                                            int64_t ld, double qlo, double qhi, const uint8_t* present,
                                            void* stream) {

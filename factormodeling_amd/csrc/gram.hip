@@ -31,6 +31,36 @@ constexpr int GKP = GK + 2;    // padded row: bank = (4 r + 2 k) mod 64, conflic
 constexpr int MK = 64;         // bf16 K chunk
 constexpr int MKP = MK + 8;    // padded row (16 B)
 
+// Tile t of the row-major upper triangle of an nb x nb tile grid: (0,0), (0,1), ...,
+// (0,nb-1), (1,1), ...  (nb <= 16 at F = 2000, so the walk is short and block-uniform.)
+__device__ __forceinline__ void upper_tile(int t, int nb, int& ti, int& tj) {
+  ti = 0;
+  while (t >= nb - ti) { t -= nb - ti; ++ti; }
+  tj = ti + t;
+}
+
+// Workspace of the wide-panel Gram (fmx_gram): the per-slice partial tiles.
+struct GramPlan {
+  int nb;
+  int64_t ntile, nslice, dps;
+  int64_t part_elems() const { return nslice * ntile * GT * GT; }
+};
+static GramPlan gram_plan(int64_t F, int64_t A, int64_t d0, int64_t d1, bool mask) {
+  GramPlan p;
+  p.nb = (int)ceil_div(F, GT);
+  p.ntile = (int64_t)p.nb * (p.nb + 1) / 2;
+  const int64_t ndates = d1 - d0;
+  // >= ~1024 workgroups to fill 256 CUs; bf16 slices must stay < 2^24 (date, asset) pairs
+  p.nslice = std::max<int64_t>(1, std::min<int64_t>(ndates, ceil_div(1024, p.ntile)));
+  p.dps = ceil_div(ndates, p.nslice);
+  if (mask) {
+    const int64_t cap = std::max<int64_t>(1, ((int64_t)1 << 24) / std::max<int64_t>(A, 1) - 1);
+    p.dps = std::min(p.dps, cap);
+  }
+  p.nslice = ceil_div(ndates, p.dps);
+  return p;
+}
+
 // per-date z-score of one (f, d) row; builder spec: mean/std(ddof=0) over non-NaN,
 // NaN -> 0, sigma in {0, NaN} -> whole row 0 and M = 0.  M is written as bf16 0/1.
 // Dates [d0, d0 + gridDim.x) of X [F][D][ld] into Z / M [F][Dout][ld] (Dout = the range
@@ -91,12 +121,13 @@ __device__ __forceinline__ void load_chunk(const double* __restrict__ row, bool 
 template <bool VEC>
 __global__ void __launch_bounds__(512)
 k_gram_f64(const double* __restrict__ Z, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
-           int64_t dates_per_slice, const int32_t* __restrict__ tile_i, const int32_t* __restrict__ tile_j,
-           int64_t ntile, double* __restrict__ part) {
+           int64_t dates_per_slice, int nb, int64_t ntile, double* __restrict__ part) {
   __shared__ double As[GT * GKP];
   __shared__ double Bs[GT * GKP];
   const int64_t tile = blockIdx.x, slice = blockIdx.y;
-  const int i0 = tile_i[tile] * GT, j0 = tile_j[tile] * GT;
+  int ti, tj;
+  upper_tile((int)tile, nb, ti, tj);
+  const int i0 = ti * GT, j0 = tj * GT;
   const int64_t ds = d0 + slice * dates_per_slice;
   const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -161,12 +192,13 @@ k_gram_f64(const double* __restrict__ Z, int64_t F, int64_t D, int64_t A, int64_
 // row = (reg&3) + 8(reg>>2) + 4(l>>5).
 __global__ void __launch_bounds__(256)
 k_gram_mask(const uint16_t* __restrict__ M, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
-            int64_t dates_per_slice, const int32_t* __restrict__ tile_i, const int32_t* __restrict__ tile_j,
-            int64_t ntile, double* __restrict__ part) {
+            int64_t dates_per_slice, int nb, int64_t ntile, double* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) uint16_t As[GT * MKP];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[GT * MKP];
   const int64_t tile = blockIdx.x, slice = blockIdx.y;
-  const int i0 = tile_i[tile] * GT, j0 = tile_j[tile] * GT;
+  int ti, tj;
+  upper_tile((int)tile, nb, ti, tj);
+  const int i0 = ti * GT, j0 = tj * GT;
   const int64_t ds = d0 + slice * dates_per_slice;
   const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -238,11 +270,12 @@ k_gram_mask(const uint16_t* __restrict__ M, int64_t F, int64_t D, int64_t A, int
 
 // Sum the slices in order and scatter the tile (and its mirror) into G[F][F].
 // grid = (tile, GT*GT/256 element chunks).
-__global__ void k_gram_reduce(const double* __restrict__ part, int64_t nslice, int64_t ntile,
-                              const int32_t* __restrict__ tile_i, const int32_t* __restrict__ tile_j, int64_t F,
+__global__ void k_gram_reduce(const double* __restrict__ part, int64_t nslice, int64_t ntile, int nb, int64_t F,
                               double* __restrict__ G, int accumulate) {
   const int64_t tile = blockIdx.x;
-  const int i0 = tile_i[tile] * GT, j0 = tile_j[tile] * GT;
+  int ti, tj;
+  upper_tile((int)tile, nb, ti, tj);
+  const int i0 = ti * GT, j0 = tj * GT;
   {
     const int e = blockIdx.y * blockDim.x + threadIdx.x;
     if (e >= GT * GT) return;
@@ -396,6 +429,125 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
   }
 }
 
+// G = Z Z^T (fp64 MFMA) + validity bits, double-buffered: the k_gram_small<NB, 0> work
+// with the chunk pipeline reorganised for MFMA occupancy.  k_gram_small's 57 KB of LDS let
+// two workgroups share a CU, so the compiler capped it at 64 VGPRs and spilled the 6
+// accumulator blocks (76 B/lane of scratch) and every chunk paid two barriers with the
+// MFMA units idle while the whole workgroup z-scored the next chunk.  Here one workgroup
+// owns a CU (amdgpu_waves_per_eu 4: 128 VGPRs, no spill), Zs is double-buffered, and each
+// iteration stages chunk c+1 into the idle buffer (VALU + LDS writes, overlapping the other
+// waves' MFMAs), issues the loads of chunk c+2, runs chunk c's MFMAs, then one barrier.
+// Slices are equal ranges of the flattened (date, 32-asset block) chunk sequence, one per
+// CU.  The row stats are double-buffered by date parity, loaded one date ahead.
+template <int NB>
+__global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
+          int64_t ld, int64_t d0, int64_t nch, int64_t total, int64_t nslice, double* __restrict__ part,
+          uint32_t* __restrict__ mbits) {
+  constexpr int FP = 16 * NB;
+  constexpr int NTRI = NB * (NB + 1) / 2;
+  constexpr int NWV = SG_NT / 64;
+  constexpr int BPW = (NTRI + NWV - 1) / NWV;
+  constexpr int NEL = FP * SG_K;
+  constexpr int EPT = (NEL + SG_NT - 1) / SG_NT;
+  __shared__ double Zs[2][FP * SG_KP];
+  __shared__ double mu_s[2][FP], sd_s[2][FP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t slice = blockIdx.x;
+  const int64_t c0 = slice * total / nslice, c1 = (slice + 1) * total / nslice;
+  int blk[BPW];
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) {
+    int j = wid + NWV * u, bi = 0;
+    blk[u] = -1;
+    if (j < NTRI) {
+      while (j >= NB - bi) { j -= NB - bi; ++bi; }
+      blk[u] = bi | ((bi + j) << 8);
+    }
+  }
+  dbl4 gacc[BPW];
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) gacc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double xr[EPT];
+  // next chunk to load (date index relative to d0, asset block), walked by counters
+  int64_t ld_d = c0 / nch, ld_a = c0 - (c0 / nch) * nch;
+  auto issue = [&]() {
+    const int64_t d = d0 + ld_d, a0 = ld_a * SG_K;
+    if (++ld_a == nch) { ld_a = 0; ++ld_d; }
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
+      const int64_t a = a0 + cl;
+      xr[u] = (e < NEL && r < F && a < A) ? X[((int64_t)r * D + d) * ld + a] : qnan();
+    }
+  };
+  auto load_stats = [&](int64_t dr) {             // date d0 + dr into buffer dr & 1
+    const int p = (int)(dr & 1);
+    for (int r = tid; r < FP; r += SG_NT) {
+      mu_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr)] : 0.0;
+      sd_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
+    }
+  };
+  // stage the chunk held in xr (global chunk index c, date dr) into buffer b
+  auto stage = [&](int64_t c, int64_t dr, int b) {
+    const int p = (int)(dr & 1);
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
+      if (e >= NEL) continue;                     // wave-uniform (NEL is a multiple of 64)
+      const double v = xr[u], sd = sd_s[p][r];
+      const bool ok = (v == v) && (sd > 0.0);
+      Zs[b][r * SG_KP + cl] = ok ? (v - mu_s[p][r]) / sd : 0.0;
+      const uint64_t bal = __ballot(ok);
+      if ((lane & 31) == 0 && r < F) mbits[(uint32_t)c * (uint32_t)F + (uint32_t)r] = (uint32_t)(bal >> lane);
+    }
+  };
+  if (c0 >= c1) return;
+  // prologue: stats of the first chunk's date (and of the next chunk's, if it starts a
+  // date), stage chunk c0, issue chunk c0 + 1
+  int64_t cur_d = c0 / nch;                       // date (relative) of chunk c
+  load_stats(cur_d);
+  if (c0 + 1 < c1 && (c0 + 1) % nch == 0) load_stats(cur_d + 1);
+  issue();
+  __syncthreads();
+  stage(c0, cur_d, 0);
+  if (c0 + 1 < c1) issue();
+  __syncthreads();
+  for (int64_t c = c0; c < c1; ++c) {
+    const int b = (int)((c - c0) & 1);
+    if (c + 1 < c1) {
+      const int64_t dn = (c + 1) / nch;           // date of chunk c + 1
+      stage(c + 1, dn, b ^ 1);                    // its stats were loaded a date ahead
+      if (c + 2 < c1) {
+        if ((c + 2) % nch == 0) load_stats(dn + 1);   // the buffer of date dn - 1: dead
+        issue();
+      }
+    }
+#pragma unroll 1
+    for (int ks = 0; ks < SG_K; ks += 4) {
+      const int kk = ks + (lane >> 4);
+#pragma unroll
+      for (int u = 0; u < BPW; ++u) {
+        if (blk[u] < 0) continue;                 // wave-uniform
+        const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+        const double a = Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
+        const double bb = Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
+        gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  double* p = part + slice * (int64_t)FP * FP;
+#pragma unroll
+  for (int u = 0; u < BPW; ++u) {
+    if (blk[u] < 0) continue;
+    const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+    const int col = bj * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[(bi * 16 + (lane >> 4) + 4 * r) * FP + col] = gacc[u][r];
+  }
+}
+
 // Sum the slices in order (deterministic) for the upper-triangle blocks and mirror.
 __global__ void k_gram_small_reduce(const double* __restrict__ partG, const double* __restrict__ partN,
                                     int64_t nslice, int FP, int64_t F, double* __restrict__ G,
@@ -464,33 +616,74 @@ k_gram_popc(const uint32_t* __restrict__ mbits, int64_t F, int64_t nw, int64_t w
   }
 }
 
-template <int NB>
-static fmx_status gram_small_launch(const double* X, const double* stats, double* G, double* N, int64_t F,
-                                    int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int accumulate,
-                                    hipStream_t st) {
-  constexpr int FP = 16 * NB;
-  const int64_t ndates = d1 - d0;
-  int64_t nslice = std::min<int64_t>(ndates, 512);
-  const int64_t dps = ceil_div(ndates, nslice);
-  nslice = ceil_div(ndates, dps);
-  double* part = nullptr;
-  const int64_t st_elems = (int64_t)FP * FP * nslice;
+// Workspace of the fused F <= 256 Gram (fmx_gram_fused), carved from the caller's buffer:
+// per-slice partial G tiles (and N tiles on the bf16-MFMA A/B path), the validity bits and
+// the 64-bit pair counters.
+struct SmallPlan {
+  int64_t FP, nslice, dps, nw;
+  bool mask_mfma;
+  int64_t part_bytes() const { return (int64_t)sizeof(double) * FP * FP * nslice * (mask_mfma ? 2 : 1); }
+  int64_t bits_bytes() const { return mask_mfma ? 0 : align256((int64_t)sizeof(uint32_t) * nw * FPF); }
+  int64_t cnt_bytes() const { return mask_mfma ? 0 : (int64_t)sizeof(unsigned long long) * FP * FP; }
+  int64_t bytes() const { return align256(part_bytes()) + bits_bytes() + cnt_bytes(); }
+  int64_t FPF;   // F (rows of the bit matrix)
+  static int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+};
+static SmallPlan small_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
+  SmallPlan p;
+  p.FP = 16 * ceil_div(std::max<int64_t>(F, 1), 16);
+  p.FPF = F;
+  const int64_t ndates = std::max<int64_t>(d1 - d0, 1);
+  p.nslice = std::min<int64_t>(ndates, 512);
+  p.dps = ceil_div(ndates, p.nslice);
+  p.nslice = ceil_div(ndates, p.dps);
   // pair counts: validity bits packed by the fp64 pass + AND/popcount (default), or the
   // bf16 MFMA pass over the panel (FMX_GRAM_MASK_MFMA=1, kept for A/B)
   static const bool mask_mfma = getenv("FMX_GRAM_MASK_MFMA") != nullptr;
-  const int64_t nchw = ceil_div(A, (int64_t)SG_K), nw = ndates * nchw;
-  uint32_t* mbits = nullptr;
-  unsigned long long* ncnt = nullptr;
-  if (mask_mfma) {
-    FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * st_elems, st));
-  } else {
-    FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * st_elems, st));
-    FMX_HIP(hipMallocAsync((void**)&mbits, sizeof(uint32_t) * F * nw, st));
-    FMX_HIP(hipMallocAsync((void**)&ncnt, sizeof(unsigned long long) * FP * FP, st));
-    FMX_HIP(hipMemsetAsync(ncnt, 0, sizeof(unsigned long long) * FP * FP, st));
+  p.mask_mfma = mask_mfma;
+  p.nw = std::max<int64_t>(d1 - d0, 0) * ceil_div(A, (int64_t)SG_K);
+  if (!mask_mfma) {
+    // k_gram_db: one slice (workgroup) per CU over equal ranges of the nw chunks
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return std::max(n, 1);
+    }();
+    p.nslice = std::max<int64_t>(1, std::min<int64_t>(p.nw, cus));
+    p.dps = 0;
   }
-  k_gram_small<NB, 0><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part, mbits);
-  FMX_LAUNCH_CHECK("k_gram_small<G>");
+  return p;
+}
+
+template <int NB>
+static fmx_status gram_small_launch(const double* X, const double* stats, double* G, double* N, int64_t F,
+                                    int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int accumulate,
+                                    char* work, hipStream_t st) {
+  constexpr int FP = 16 * NB;
+  const SmallPlan pl = small_plan(F, A, d0, d1);
+  const int64_t nslice = pl.nslice, dps = pl.dps, nw = pl.nw;
+  const int64_t st_elems = (int64_t)FP * FP * nslice;
+  const bool mask_mfma = pl.mask_mfma;
+  double* part = reinterpret_cast<double*>(work);
+  uint32_t* mbits = mask_mfma ? nullptr : reinterpret_cast<uint32_t*>(work + SmallPlan::align256(pl.part_bytes()));
+  unsigned long long* ncnt =
+      mask_mfma ? nullptr
+                : reinterpret_cast<unsigned long long*>(work + SmallPlan::align256(pl.part_bytes()) + pl.bits_bytes());
+  if (ncnt) FMX_HIP(hipMemsetAsync(ncnt, 0, sizeof(unsigned long long) * FP * FP, st));
+  static const bool db = getenv("FMX_GRAM_SINGLE_BUFFER") == nullptr;   // A/B switch
+  if (!mask_mfma && db) {
+    const int64_t nch = ceil_div(A, (int64_t)SG_K);
+    k_gram_db<NB><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits);
+    FMX_LAUNCH_CHECK("k_gram_db");
+  } else {
+    const int64_t dps2 = mask_mfma ? dps : ceil_div(d1 - d0, nslice);
+    const int64_t ns2 = mask_mfma ? nslice : ceil_div(d1 - d0, dps2);
+    k_gram_small<NB, 0><<<(unsigned)ns2, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps2, part, mbits);
+    FMX_LAUNCH_CHECK("k_gram_small<G>");
+    if (!mask_mfma && ns2 < nslice)   // fewer date slices than planned: zero the unused partials
+      FMX_HIP(hipMemsetAsync(part + ns2 * FP * FP, 0, sizeof(double) * (nslice - ns2) * FP * FP, st));
+  }
   if (mask_mfma) {
     k_gram_small<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps, part + st_elems,
                                                            nullptr);
@@ -507,9 +700,6 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(
       part, mask_mfma ? part + st_elems : nullptr, nslice, FP, F, G, N, accumulate, mask_mfma ? nullptr : ncnt);
   FMX_LAUNCH_CHECK("k_gram_small_reduce");
-  FMX_HIP(hipFreeAsync(part, st));
-  if (mbits) FMX_HIP(hipFreeAsync(mbits, st));
-  if (ncnt) FMX_HIP(hipFreeAsync(ncnt, st));
   return FMX_OK;
 }
 
@@ -566,23 +756,34 @@ k_window_prune(const double* __restrict__ partG, const double* __restrict__ part
   for (int i = lane; i < nk; i += 64) w[kept[i]] = 1.0 / (double)nk;
 }
 
-template <int NB>
-static fmx_status window_prune_launch(const double* X, const double* stats, int64_t F, int64_t D, int64_t A,
-                                      int64_t ld, int64_t J, int W, const int32_t* s0_host, const int32_t* order,
-                                      const double* metrics, int col, double thr, double rho, int top_x,
-                                      double* w_out, hipStream_t st) {
-  constexpr int FP = 16 * NB;
-  int64_t d_lo = D, d_hi = 0;
+// Workspace of fmx_corr_prune_windows: per-date G and N partials over the dates the
+// windows touch, then the window starts.
+static void prune_dates(int64_t D, int64_t J, int W, const int32_t* s0_host, int64_t& d_lo, int64_t& nd) {
+  d_lo = D;
+  int64_t d_hi = 0;
   for (int64_t j = 0; j < J; ++j) {
     d_lo = std::min<int64_t>(d_lo, std::max<int64_t>(0, s0_host[j]));
     d_hi = std::max<int64_t>(d_hi, std::min<int64_t>(D, (int64_t)s0_host[j] + W));
   }
   if (d_hi <= d_lo) d_hi = d_lo = 0;
-  const int64_t nd = d_hi - d_lo;
-  double* part = nullptr;
-  int32_t* s0 = nullptr;
-  FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * 2 * std::max<int64_t>(nd, 1) * FP * FP, st));
-  FMX_HIP(hipMallocAsync((void**)&s0, sizeof(int32_t) * J, st));
+  nd = d_hi - d_lo;
+}
+static int64_t prune_part_bytes(int64_t F, int64_t nd) {
+  const int64_t FP = 16 * ceil_div(std::max<int64_t>(F, 1), 16);
+  return SmallPlan::align256((int64_t)sizeof(double) * 2 * std::max<int64_t>(nd, 1) * FP * FP);
+}
+
+template <int NB>
+static fmx_status window_prune_launch(const double* X, const double* stats, int64_t F, int64_t D, int64_t A,
+                                      int64_t ld, int64_t J, int W, const int32_t* s0_host, const int32_t* order,
+                                      const double* metrics, int col, double thr, double rho, int top_x,
+                                      double* w_out, char* work, hipStream_t st) {
+  constexpr int FP = 16 * NB;
+  int64_t d_lo, nd;
+  prune_dates(D, J, W, s0_host, d_lo, nd);
+  const int64_t d_hi = d_lo + nd;
+  double* part = reinterpret_cast<double*>(work);
+  int32_t* s0 = reinterpret_cast<int32_t*>(work + prune_part_bytes(F, nd));
   FMX_HIP(hipMemcpyAsync(s0, s0_host, sizeof(int32_t) * J, hipMemcpyHostToDevice, st));
   if (nd > 0) {
     // one slice per date: the partials ARE the per-date Grams (G on fp64 MFMA, N on bf16)
@@ -595,8 +796,6 @@ static fmx_status window_prune_launch(const double* X, const double* stats, int6
   k_window_prune<<<(unsigned)J, 64, sizeof(int) * F, st>>>(part, part + nd * FP * FP, FP, F, d_lo, nd, W, s0, order,
                                                           metrics, col, thr, rho, top_x, w_out);
   FMX_LAUNCH_CHECK("k_window_prune");
-  FMX_HIP(hipFreeAsync(part, st));
-  FMX_HIP(hipFreeAsync(s0, st));
   FMX_HIP(hipStreamSynchronize(st));              // s0_host may be a temporary
   return FMX_OK;
 }
@@ -605,9 +804,23 @@ static fmx_status window_prune_launch(const double* X, const double* stats, int6
 
 using namespace fmx;
 
+static fmx_status check_work(const void* work, int64_t work_bytes, int64_t need, const char* query) {
+  if (need > 0 && (!work || work_bytes < need)) {
+    set_error(std::string("workspace smaller than ") + query + "()");
+    return FMX_ERR_ARG;
+  }
+  return FMX_OK;
+}
+
+extern "C" int64_t fmx_gram_fused_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
+  (void)D;
+  if (F <= 0 || F > 256 || d1 <= d0) return 0;
+  return small_plan(F, A, d0, d1).bytes();
+}
+
 extern "C" fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F,
                                      int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate,
-                                     void* stream) {
+                                     void* work, int64_t work_bytes, void* stream) {
   FMX_ARG(X && stats && G && N, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
   if (F > 256) {
@@ -615,11 +828,15 @@ extern "C" fmx_status fmx_gram_fused(const double* X, const double* stats, doubl
     return FMX_ERR_UNSUPPORTED;
   }
   if (F == 0 || d1 == d0) return FMX_OK;
+  if (fmx_status e = check_work(work, work_bytes, fmx_gram_fused_work_bytes(F, D, A, d0, d1),
+                                "fmx_gram_fused_work_bytes"))
+    return e;
   hipStream_t st = as_stream(stream);
+  char* w = static_cast<char*>(work);
   const int nb = (int)ceil_div(F, 16);
   switch (nb) {
 #define FMX_GS(K) \
-  case K: return gram_small_launch<K>(X, stats, G, N, F, D, A, ld, d0, d1, accumulate, st);
+  case K: return gram_small_launch<K>(X, stats, G, N, F, D, A, ld, d0, d1, accumulate, w, st);
     FMX_GS(1) FMX_GS(2) FMX_GS(3) FMX_GS(4) FMX_GS(5) FMX_GS(6) FMX_GS(7) FMX_GS(8)
     FMX_GS(9) FMX_GS(10) FMX_GS(11) FMX_GS(12) FMX_GS(13) FMX_GS(14) FMX_GS(15) FMX_GS(16)
 #undef FMX_GS
@@ -650,66 +867,63 @@ extern "C" fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uin
 }
 
 static fmx_status gram_run(const void* Zp, bool mask, double* G, int64_t F, int64_t D, int64_t A, int64_t ld,
-                           int64_t d0, int64_t d1, int accumulate, hipStream_t st) {
-  const int nb = (int)ceil_div(F, GT);
-  std::vector<int32_t> packed;
-  for (int i = 0; i < nb; ++i)
-    for (int j = i; j < nb; ++j) packed.push_back(i);
-  const int64_t ntile = (int64_t)packed.size();
-  for (int i = 0; i < nb; ++i)
-    for (int j = i; j < nb; ++j) packed.push_back(j);
-  const int64_t ndates = d1 - d0;
-  // >= ~1024 workgroups to fill 256 CUs; bf16 slices must stay < 2^24 (date, asset) pairs
-  int64_t nslice = std::max<int64_t>(1, std::min<int64_t>(ndates, ceil_div(1024, ntile)));
-  int64_t dps = ceil_div(ndates, nslice);
+                           int64_t d0, int64_t d1, int accumulate, double* part, hipStream_t st) {
+  const GramPlan pl = gram_plan(F, A, d0, d1, mask);
+  dim3 grid((unsigned)pl.ntile, (unsigned)pl.nslice);
   if (mask) {
-    const int64_t cap = std::max<int64_t>(1, ((int64_t)1 << 24) / std::max<int64_t>(A, 1) - 1);
-    dps = std::min(dps, cap);
-  }
-  nslice = ceil_div(ndates, dps);
-  int32_t* tdev = nullptr;
-  double* part = nullptr;
-  FMX_HIP(hipMallocAsync((void**)&tdev, sizeof(int32_t) * 2 * ntile, st));
-  FMX_HIP(hipMallocAsync((void**)&part, sizeof(double) * nslice * ntile * GT * GT, st));
-  FMX_HIP(hipMemcpyAsync(tdev, packed.data(), sizeof(int32_t) * 2 * ntile, hipMemcpyHostToDevice, st));
-  FMX_HIP(hipStreamSynchronize(st));  // packed is a host temporary
-  dim3 grid((unsigned)ntile, (unsigned)nslice);
-  if (mask) {
-    k_gram_mask<<<grid, 256, 0, st>>>((const uint16_t*)Zp, F, D, A, ld, d0, d1, dps, tdev, tdev + ntile, ntile, part);
+    k_gram_mask<<<grid, 256, 0, st>>>((const uint16_t*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_mask");
   } else if (ld % 2 == 0) {
-    k_gram_f64<true><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, dps, tdev, tdev + ntile, ntile,
-                                           part);
+    k_gram_f64<true><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_f64");
   } else {
-    k_gram_f64<false><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, dps, tdev, tdev + ntile, ntile,
-                                            part);
+    k_gram_f64<false><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_f64");
   }
-  k_gram_reduce<<<dim3((unsigned)ntile, GT * GT / 256), 256, 0, st>>>(part, nslice, ntile, tdev, tdev + ntile, F, G,
-                                                                      accumulate);
+  k_gram_reduce<<<dim3((unsigned)pl.ntile, GT * GT / 256), 256, 0, st>>>(part, pl.nslice, pl.ntile, pl.nb, F, G,
+                                                                        accumulate);
   FMX_LAUNCH_CHECK("k_gram_reduce");
-  FMX_HIP(hipFreeAsync(part, st));
-  FMX_HIP(hipFreeAsync(tdev, st));
   return FMX_OK;
 }
 
+extern "C" int64_t fmx_gram_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int32_t with_mask) {
+  (void)D;
+  if (F <= 0 || d1 <= d0) return 0;
+  int64_t b = gram_plan(F, A, d0, d1, false).part_elems();
+  if (with_mask) b = std::max(b, gram_plan(F, A, d0, d1, true).part_elems());
+  return (int64_t)sizeof(double) * b;   // G then N reuse one partials buffer (stream-ordered)
+}
+
 extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, int64_t F, int64_t D,
-                               int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream) {
+                               int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,
+                               int64_t work_bytes, void* stream) {
   FMX_ARG(Z && G, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
   if (F == 0 || d1 == d0) return FMX_OK;
+  const bool with_mask = M && N;
+  if (fmx_status e = check_work(work, work_bytes, fmx_gram_work_bytes(F, D, A, d0, d1, with_mask),
+                                "fmx_gram_work_bytes"))
+    return e;
   hipStream_t st = as_stream(stream);
-  fmx_status e = gram_run(Z, false, G, F, D, A, ld, d0, d1, accumulate, st);
-  if (e || !M || !N) return e;
-  return gram_run(M, true, N, F, D, A, ld, d0, d1, accumulate, st);
+  double* part = static_cast<double*>(work);
+  fmx_status e = gram_run(Z, false, G, F, D, A, ld, d0, d1, accumulate, part, st);
+  if (e || !with_mask) return e;
+  return gram_run(M, true, N, F, D, A, ld, d0, d1, accumulate, part, st);
+}
+
+extern "C" int64_t fmx_corr_prune_windows_work_bytes(int64_t F, int64_t D, int64_t J, int32_t window,
+                                                     const int32_t* s0_host) {
+  if (F <= 0 || J <= 0 || !s0_host) return 0;
+  int64_t d_lo, nd;
+  prune_dates(D, J, window, s0_host, d_lo, nd);
+  return prune_part_bytes(F, nd) + (int64_t)sizeof(int32_t) * J;
 }
 
 extern "C" fmx_status fmx_corr_prune_windows(const double* X, const double* stats, int64_t F, int64_t D, int64_t A,
                                              int64_t ld, int64_t J, int32_t window, const int32_t* s0_host,
                                              const int32_t* order, const double* metrics, int32_t use_rank_icir,
                                              double threshold, double rho, int32_t top_x, double* w_out,
-                                             void* stream) {
+                                             void* work, int64_t work_bytes, void* stream) {
   FMX_ARG(X && stats && s0_host && order && metrics && w_out, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && J >= 0 && window >= 1 && top_x >= 0, "bad dims");
   if (F > 256) {
@@ -718,14 +932,18 @@ extern "C" fmx_status fmx_corr_prune_windows(const double* X, const double* stat
   }
   if (F == 0 || J == 0) return FMX_OK;
   FMX_ARG(J <= 0x7fffffffll, "too many windows");
+  if (fmx_status e = check_work(work, work_bytes, fmx_corr_prune_windows_work_bytes(F, D, J, window, s0_host),
+                                "fmx_corr_prune_windows_work_bytes"))
+    return e;
   hipStream_t st = as_stream(stream);
+  char* w = static_cast<char*>(work);
   const int col = use_rank_icir ? 3 : 1;
   const int nb = (int)ceil_div(F, 16);
   switch (nb) {
 #define FMX_WP(K)                                                                                            \
   case K:                                                                                                    \
     return window_prune_launch<K>(X, stats, F, D, A, ld, J, window, s0_host, order, metrics, col, threshold, \
-                                  rho, top_x, w_out, st);
+                                  rho, top_x, w_out, w, st);
     FMX_WP(1) FMX_WP(2) FMX_WP(3) FMX_WP(4) FMX_WP(5) FMX_WP(6) FMX_WP(7) FMX_WP(8)
     FMX_WP(9) FMX_WP(10) FMX_WP(11) FMX_WP(12) FMX_WP(13) FMX_WP(14) FMX_WP(15) FMX_WP(16)
 #undef FMX_WP

@@ -25,16 +25,18 @@ namespace fmx {
 
 constexpr int IC_NT = 256;
 
+struct IcLags { int32_t v[8]; };   // passed by value: no device copy of the host lag list
+
 __global__ void __launch_bounds__(IC_NT)
 k_ic_daily(const double* __restrict__ X, const double* __restrict__ R, int64_t F, int64_t D, int64_t A,
-           int64_t ld, const int32_t* __restrict__ lags, int P, double* __restrict__ out) {
+           int64_t ld, IcLags lags, int P, double* __restrict__ out) {
   extern __shared__ uint64_t keys[];
   uint16_t* idx = (uint16_t*)(keys + P);
   double* dscr = (double*)(((uintptr_t)(idx + P) + 15) & ~(uintptr_t)15);
   int* iscr = (int*)(dscr + 16);
   const int64_t t = blockIdx.x, f = blockIdx.y;
   const int li = blockIdx.z;
-  const int L = lags[li];
+  const int L = lags.v[li];
   double* o_n = out + ((int64_t)(li * 4 + 0) * F + f) * D + t;
   double* o_ic = out + ((int64_t)(li * 4 + 1) * F + f) * D + t;
   double* o_ric = out + ((int64_t)(li * 4 + 2) * F + f) * D + t;
@@ -309,18 +311,13 @@ extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, 
     set_error("A too large for the IC kernels' LDS (A <= 12288; longer rows: fmx_ic_daily_ranked)");
     return FMX_ERR_UNSUPPORTED;
   }
-  int32_t* lags_dev = nullptr;
+  IcLags lv{};
+  for (int i = 0; i < n_lags; ++i) lv.v[i] = lags[i];
   hipStream_t st = as_stream(stream);
-  FMX_HIP(hipMallocAsync((void**)&lags_dev, sizeof(int32_t) * n_lags, st));
-  FMX_HIP(hipMemcpyAsync(lags_dev, lags, sizeof(int32_t) * n_lags, hipMemcpyHostToDevice, st));
-  FMX_HIP(hipStreamSynchronize(st));
   if (lds > 64 * 1024)
     FMX_HIP(hipFuncSetAttribute((const void*)k_ic_daily, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  void* args[] = {(void*)&X, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&lags_dev, (void*)&P,
-                  (void*)&out};
-  FMX_HIP(hipLaunchKernel((const void*)k_ic_daily, dim3((unsigned)D, (unsigned)F, (unsigned)n_lags), dim3(IC_NT),
-                          args, lds, st));
-  FMX_HIP(hipFreeAsync(lags_dev, st));
+  k_ic_daily<<<dim3((unsigned)D, (unsigned)F, (unsigned)n_lags), IC_NT, lds, st>>>(X, R, F, D, A, ld, lv, P, out);
+  FMX_LAUNCH_CHECK("k_ic_daily");
   return FMX_OK;
 }
 

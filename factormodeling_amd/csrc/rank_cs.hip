@@ -56,6 +56,28 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   return FMX_OK;
 }
 
+// Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
+// raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
+fmx_status br_cs_rank2(const double* X, uint32_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
+  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
+  const int E = br_emax(A, nt_fa);
+  const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense)(nt_fa, E);
+  if (!k || !lds_fits(k, lds_fr)) { set_error("fmx_cs_rank2: A <= 16384"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D == 0) return FMX_OK;
+  double* Y = nullptr;
+  double* Y2 = nullptr;
+  int method = FMX_RANK_AVERAGE;
+  const uint8_t* present = nullptr;
+  double qlo = 0.0, qhi = 0.0;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK};
+  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  return FMX_OK;
+}
+
 }  // namespace fmx
 
 BR_PHASE_EXPORT(fmx_debug_phase_cs)

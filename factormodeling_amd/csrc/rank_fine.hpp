@@ -110,9 +110,11 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       (method != FMX_RANK_AVERAGE_PROPAGATE && nrow == 1)) {
     // scipy propagate: one NaN -> all NaN; single-row date -> 0.5 (operations.py:58)
     const bool half = (method != FMX_RANK_AVERAGE_PROPAGATE) && nrow == 1;
+    if (Y) {                                  // Y == NULL: doubled ranks only (fmx_cs_rank2)
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k)
-      if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+      for (int k = 0; k < EMAX; ++k)
+        if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+    }
     if (RK) {                                 // nv == 0 or a single-row date (rank 1)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
@@ -208,7 +210,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (method == FMX_RANK_MIN) r = (double)(less + 1);
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
-    y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
+    if (Y) y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
     if (RK) RK[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
 #pragma unroll

@@ -325,6 +325,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
                       const uint8_t* present, hipStream_t st);
 fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
                              double qlo, double qhi, const uint8_t* present, uint32_t* RK, hipStream_t st);
+fmx_status br_cs_rank2(const double* X, uint32_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st);
 fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                           double qlo, double qhi, const uint8_t* present, hipStream_t st);
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,

@@ -153,12 +153,21 @@ _WORK = {}
 
 
 def _workspace(device, n):
-    """Per-device int32 scratch reused across calls (grown on demand; ops on one stream)."""
-    w = _WORK.get(device)
+    """Device scratch of >= n int32 words for the library calls that take a workspace
+    (fmx_*_work_len / fmx_*_work_bytes): one buffer per (device, stream), grown on demand
+    and reused, so the hot path never allocates.  Calls on one stream are ordered, so
+    consecutive ops share it safely; another stream gets its own buffer."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    w = _WORK.get(key)
     if w is None or w.numel() < n:
         w = torch.empty(max(n, 1), dtype=torch.int32, device=device)
-        _WORK[device] = w
+        _WORK[key] = w
     return w
+
+
+def _workspace_bytes(device, nbytes):
+    n = (int(nbytes) + 3) // 4
+    return _workspace(device, n), 4 * max(n, 1)
 
 
 def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None, rank2=None):
@@ -176,6 +185,20 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
     call("fmx_cs_rank_winsor", ptr(X), ptr(Yr), ptr(Yw), F, D, A, A, float(qlo), float(qhi), ptr(present),
          ptr(rank2), stream_ptr())
     return Yr, Yw
+
+
+def cs_rank2(X, rank2=None):
+    """Doubled average ranks only (fmx_cs_rank2): the rank pass ``ic_daily(..., rank2=)``
+    starts from when no operator output of the rows is wanted (dense rows, A <= 16384)."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if rank2 is None:
+        rank2 = torch.empty((F, D, A), dtype=torch.int32, device=X.device)
+    elif rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+        raise _lib.FmxError("rank2 must be a contiguous int32 [F][D][A] tensor")
+    call("fmx_cs_rank2", ptr(X), ptr(rank2), F, D, A, A, stream_ptr())
+    return rank2
 
 
 def cs_rank(X, method="average", present=None, out=None):
@@ -308,7 +331,9 @@ def gram(Z, M=None, d0=0, d1=None):
     d1 = D if d1 is None else d1
     G = torch.empty((F, F), dtype=F64, device=Z.device)
     N = torch.empty((F, F), dtype=F64, device=Z.device) if M is not None else None
-    call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, stream_ptr())
+    nb = int(_lib.load().fmx_gram_work_bytes(F, D, A, int(d0), int(d1), int(M is not None)))
+    work, wb = _workspace_bytes(Z.device, nb)
+    call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, ptr(work), wb, stream_ptr())
     return G, N
 
 
@@ -325,7 +350,10 @@ def gram_fused(X, stats, d0=0, d1=None):
     d1 = D if d1 is None else d1
     G = torch.empty((F, F), dtype=F64, device=X.device)
     N = torch.empty((F, F), dtype=F64, device=X.device)
-    call("fmx_gram_fused", ptr(X), ptr(stats), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, stream_ptr())
+    nb = int(_lib.load().fmx_gram_fused_work_bytes(F, D, A, int(d0), int(d1)))
+    work, wb = _workspace_bytes(X.device, nb)
+    call("fmx_gram_fused", ptr(X), ptr(stats), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, ptr(work), wb,
+         stream_ptr())
     return G, N
 
 
@@ -353,7 +381,9 @@ def gram_chunked(X, d0=0, d1=None, chunk=None):
             Z = torch.empty((F, n, A), dtype=F64, device=X.device)
             M = torch.empty((F, n, A), dtype=torch.bfloat16, device=X.device)
         call("fmx_zscore_exposures_range", ptr(X), ptr(Z), ptr(M), F, D, A, A, c0, c1, stream_ptr())
-        call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, n, A, A, 0, n, 1, stream_ptr())
+        nb = int(_lib.load().fmx_gram_work_bytes(F, n, A, 0, n, 1))
+        work, wb = _workspace_bytes(X.device, nb)
+        call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, n, A, A, 0, n, 1, ptr(work), wb, stream_ptr())
     return G, N
 
 
@@ -383,9 +413,12 @@ def corr_prune_windows(X, stats, metrics, order, window: int, s0, use_rank_icir=
     s0h = (ctypes.c_int32 * J)(*[int(v) for v in s0])
     w = torch.empty((J, F), dtype=F64, device=X.device)
     top = F if top_x is None else int(top_x)
-    call("fmx_corr_prune_windows", ptr(X), ptr(stats.contiguous()), F, D, A, A, J, int(window),
-         ctypes.cast(s0h, ctypes.c_void_p), ptr(order.contiguous()), ptr(metrics.contiguous()), int(bool(use_rank_icir)),
-         float(threshold), float(rho), top, ptr(w), stream_ptr())
+    s0p = ctypes.cast(s0h, ctypes.c_void_p)
+    nb = int(_lib.load().fmx_corr_prune_windows_work_bytes(F, D, J, int(window), s0p))
+    work, wb = _workspace_bytes(X.device, nb)
+    call("fmx_corr_prune_windows", ptr(X), ptr(stats.contiguous()), F, D, A, A, J, int(window), s0p,
+         ptr(order.contiguous()), ptr(metrics.contiguous()), int(bool(use_rank_icir)), float(threshold), float(rho),
+         top, ptr(w), ptr(work), wb, stream_ptr())
     return w
 
 

@@ -52,6 +52,7 @@ class StepConfig:
     factor_chunk: int = 0      # ret_ops run over chunks of this many factors (memory)
     composite: object = None   # "zscore" | "rank": weighted composite of the day's selection
     names: object = None       # factor names (composite suffix / prefix rules)
+    rank_pass: bool = False    # no op stage ranks X: rank it once (cs_rank2) for the daily IC
 
     @property
     def lookback(self):
@@ -76,7 +77,7 @@ def workload_config(name):
         return StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None)
     if name == "c5":
         return StepConfig(ops=[], ic_lags=(1, 2), select=True, gram=False, ret_ops=[("corr", 60), ("std", 60)],
-                          factor_chunk=100, composite="zscore")
+                          factor_chunk=100, composite="zscore", rank_pass=True)
     raise ValueError(f"unknown workload {name!r}")
 
 
@@ -229,6 +230,11 @@ class EngineBackend:
 
     ranked_ic_max_a = E.RANKED_IC_MAX_A
 
+    @staticmethod
+    def cs_rank2(X, rank2):
+        """The doubled ranks alone (no operator output): the IC's rank pass."""
+        E.cs_rank2(X, rank2)
+
     def op(self, kind, op, w, X, out):
         if kind == "ts":
             return E.ts(op, X, w, None, out=out)
@@ -369,6 +375,16 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
                           own=slice(sp.halo, None), side=side)
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
+    if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
+            and sp.A <= be.ranked_ic_max_a):
+        # no operator ranked X this step: one ranks-only pass feeds the wave IC
+        t0 = _ev(timers)
+        rk = getattr(sp, "rank2", None)
+        if rk is None:
+            rk = torch.empty(sp.X.shape, dtype=torch.int32, device=sp.X.device)
+        be.cs_rank2(sp.X, rk)
+        side["rank2"] = rk
+        _rec(timers, "rank2", t0)
     # daily IC for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     lags = tuple(cfg.ic_lags)

@@ -18,8 +18,11 @@
  *     groupby('symbol') + rolling/shift); cross-sectional ops reduce over the present
  *     rows of a date.  Outputs at absent cells are NaN.
  *   - stream: a hipStream_t passed as void* (NULL = default stream).  All calls are
- *     stream-ordered and asynchronous; no call allocates with hipMalloc on the hot
- *     path except the first use of a row length (pairwise-sum schedules are cached).
+ *     stream-ordered and asynchronous; no call allocates on the hot path (the only
+ *     hipMalloc is the one-time cache of a row length's pairwise-sum schedule).
+ *   - Scratch: calls that need device scratch take (work, work_bytes) from the caller,
+ *     sized by the matching fmx_*_work_bytes / fmx_*_work_len query; one buffer may be
+ *     reused by every call on the same stream.
  *   - Errors: every call returns an fmx_status; fmx_last_error() gives a thread-local
  *     message.  No exceptions cross the ABI.
  */
@@ -149,6 +152,11 @@ fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t
 fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
                               int64_t ld, double qlo, double qhi, const uint8_t* present, uint32_t* rank2,
                               void* stream);
+/* Only the doubled average ranks of fmx_cs_rank_winsor (rank2 [F][D][ld] uint32, A <=
+ * 16384): the rank pass of a daily IC over raw factors (fmx_ic_daily_ranked) when no
+ * operator output of the same rows is wanted (factor_selector.py:36-48's rankdata). */
+fmx_status fmx_cs_rank2(const double* X, uint32_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
+                        void* stream);
 /* cs_winsor (operations.py:64-68); qlo/qhi are the fractions numpy sees
  * (pandas passes q*100 and numpy divides by 100). */
 fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, double qlo,
@@ -209,13 +217,19 @@ fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uint16_t* M, i
  * (v_mfma_f64_16x16x4_f64) and N[F][F] (+)= the same sum over M on bf16 MFMA (exact
  * pair counts).  accumulate = 0 overwrites.  M/N may be NULL. */
 fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
-                    int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
+                    int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work, int64_t work_bytes,
+                    void* stream);
+/* Device workspace fmx_gram needs for these dims (with_mask: M and N given). */
+int64_t fmx_gram_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int32_t with_mask);
 /* Fused form for F <= 256: G and N straight from the raw panel X with the row stats of
  * fmx_cs_moment_stats (z = (x - mean) / sd where x is non-NaN and sd > 0, else 0; M the
  * same validity), one pass over X, both MFMA products in the same workgroup.  Returns
  * FMX_ERR_UNSUPPORTED for F > 256 (use fmx_zscore_exposures + fmx_gram). */
 fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F, int64_t D,
-                          int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* stream);
+                          int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,
+                          int64_t work_bytes, void* stream);
+/* Device workspace fmx_gram_fused needs (per-slice partial tiles, validity bits, counts). */
+int64_t fmx_gram_fused_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1);
 /* The builder-defined corr_prune selector for J rolling windows in one call:
  * per-date Gram partials of the raw panel X (z-scored with stats [F][D][2] from
  * fmx_cs_moment_stats) for every date any window touches, then per window j the pooled
@@ -226,7 +240,9 @@ fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, doubl
 fmx_status fmx_corr_prune_windows(const double* X, const double* stats, int64_t F, int64_t D, int64_t A, int64_t ld,
                                   int64_t J, int32_t window, const int32_t* s0_host, const int32_t* order,
                                   const double* metrics, int32_t use_rank_icir, double threshold, double rho,
-                                  int32_t top_x, double* w_out, void* stream);
+                                  int32_t top_x, double* w_out, void* work, int64_t work_bytes, void* stream);
+/* Device workspace fmx_corr_prune_windows needs (per-date partials of the touched dates). */
+int64_t fmx_corr_prune_windows_work_bytes(int64_t F, int64_t D, int64_t J, int32_t window, const int32_t* s0_host);
 
 /* ---- composite factors (composite_factor.py:137-342) ------------------------------- */
 /* composite_factor_calculation preprocessing (:157-178): Adj[k] = suffix-scaled X[cols[k]]
