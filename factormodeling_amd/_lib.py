@@ -31,6 +31,8 @@ SIGNATURES = {
     "fmx_cs_moment_stats": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_zscore_neutralize": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
     "fmx_cs_rank_winsor": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp, c_vp],
+    "fmx_cs_rank_sorted": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp],
+    "fmx_cs_rank_sorted_work_bytes": [c_i64, c_i64, c_i64],
     "fmx_cs_rank2": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
@@ -69,7 +71,8 @@ SIGNATURES = {
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
-             "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64}
+             "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
+             "fmx_cs_rank_sorted_work_bytes": c_i64}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)

@@ -163,7 +163,7 @@ constexpr int CSR_EL = 16;            // elements per lane: leaves hold <= 128 =
 template <int OP>
 __global__ void __launch_bounds__(CSR_NT, 8)
 k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
-               PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2) {
+               PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2, int nts) {
   __shared__ int32_t sch[PW_LDS_MAX];
   __shared__ double nodes[2 * (CSR_NT / 8) + 8];
   __shared__ int iscr[CSR_NT / 64 + 2];
@@ -267,9 +267,13 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
         return (t - mean) / sd;
       };
       double* y = Y + row * ld;
+      auto put = [&](double v, double* p) {   // nts: write-once outputs as nontemporal stores
+        if (nts) __builtin_nontemporal_store(v, p);
+        else *p = v;
+      };
 #pragma unroll
       for (int i = 0; i < CSR_EL; ++i)
-        if (i < nfull) y[st + j + 8 * i] = outv(xv[i]);
+        if (i < nfull) put(outv(xv[i]), y + st + j + 8 * i);
       if (act && j == 0)
         for (int q = stop; q < len; ++q) y[st + q] = outv(x[st + q]);
       if (OP == FMX_CS_ZSCORE && Y2) {
@@ -278,7 +282,7 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
         double* y2 = Y2 + row * ld;
 #pragma unroll
         for (int i = 0; i < CSR_EL; ++i)
-          if (i < nfull) y2[st + j + 8 * i] = g2 ? 0.0 : outv(xv[i]);
+          if (i < nfull) put(g2 ? 0.0 : outv(xv[i]), y2 + st + j + 8 * i);
         if (act && j == 0)
           for (int q = stop; q < len; ++q) y2[st + q] = g2 ? 0.0 : outv(x[st + q]);
       }
@@ -708,8 +712,9 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
       }
       const int64_t nrows = F * D;
       const int64_t grid = std::min<int64_t>(nrows, slots);
+      static const int nts = getenv("FMX_CS_NT") ? atoi(getenv("FMX_CS_NT")) : 0;   // A/B: nontemporal stores
       void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
-                       (void*)&stats, (void*)&Y2};
+                       (void*)&stats, (void*)&Y2, (void*)&nts};
       FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
       return FMX_OK;
     }

@@ -210,8 +210,10 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (method == FMX_RANK_MIN) r = (double)(less + 1);
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
-    if (Y) y[t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den;
-    if (RK) RK[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1);
+    // write-once outputs: nontemporal stores
+    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den, y + t + k * NT);
+    if (RK) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1),
+                                        RK + row * ld + t + k * NT);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -240,7 +242,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
       double o = v;
       if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
-      y2[t + k * NT] = (PRES && !((pm >> k) & 1)) ? qnan() : o;
+      __builtin_nontemporal_store((PRES && !((pm >> k) & 1)) ? qnan() : o, y2 + t + k * NT);
     }
   }
   BR_PH();

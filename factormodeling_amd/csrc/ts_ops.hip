@@ -193,8 +193,8 @@ __device__ __forceinline__ double ts_step(ColState& c, double v, int W, double* 
       // oldest element sits at `slot` (just advanced); weights 1..W oldest->newest
       double acc = 0.0;
       int sl = c.slot;
-      for (int k = 1; k <= W; ++k) {
-        acc += ring[((int64_t)sl * TS_BLOCK + lane) * V + u] * (double)k;
+      for (int k = 1; k <= W; ++k) {   // fused multiply-adds, as numpy's BLAS ddot
+        acc = __builtin_fma(ring[((int64_t)sl * TS_BLOCK + lane) * V + u], (double)k, acc);
         sl = (sl + 1 == W) ? 0 : sl + 1;
       }
       out = acc / ((double)W * (double)(W + 1) / 2.0);
@@ -260,7 +260,7 @@ __device__ __forceinline__ double ts_step_reg(ColState& c, double v, double* rin
       // oldest element sits in slot q+1 (mod W); weights 1..W oldest->newest
       double acc = 0.0;
 #pragma unroll
-      for (int k = 1; k <= W; ++k) acc += ring[(q + k) % W] * (double)k;
+      for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);   // as BLAS ddot
       out = acc / ((double)W * (double)(W + 1) / 2.0);
     }
   } else if (OP == FMX_TS_DIFF) {
@@ -360,9 +360,11 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
   c.ms.add(v); c.vs.add(v);
   const double m = c.ms.result(W);
   const double sd = zsqrt(c.vs.var(W, 1));
-  if (Ym) Ym[off] = m;
-  if (Ys) Ys[off] = sd;
-  if (Yz) Yz[off] = (v - m) / (sd == 0.0 ? qnan() : sd);
+  // outputs are written once and not re-read by this kernel: nontemporal (streaming)
+  // stores, +11 % on this 1-read / 5-write column walk (tools/colwalk.hip)
+  if (Ym) __builtin_nontemporal_store(m, Ym + off);
+  if (Ys) __builtin_nontemporal_store(sd, Ys + off);
+  if (Yz) __builtin_nontemporal_store((v - m) / (sd == 0.0 ? qnan() : sd), Yz + off);
   if (full && old != old) c.nan_w -= 1;
   if (c.i >= WR && oldr != oldr) c.nan_r -= 1;
   if (v != v) { c.nan_w += 1; c.nan_r += 1; }
@@ -378,17 +380,17 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
       }
       o = ((double)less + (double)(eq + 1) / 2.0) / (double)WR;
     }
-    Yr[off] = o;
+    __builtin_nontemporal_store(o, Yr + off);
   }
   if (Yd) {
     double o = qnan();
     if (c.i + 1 >= W && c.nan_w == 0) {
       double acc = 0.0;
 #pragma unroll
-      for (int k = 1; k <= W; ++k) acc += ring[(q + k) % W] * (double)k;
+      for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);
       o = acc / ((double)W * (double)(W + 1) / 2.0);
     }
-    Yd[off] = o;
+    __builtin_nontemporal_store(o, Yd + off);
   }
   c.i += 1;
   __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps' live ranges apart
@@ -411,7 +413,7 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
   for (int q = 0; q < W; ++q) ring[q] = 0.0;
   double pf[PF];
 #pragma unroll
-  for (int q = 0; q < PF; ++q) pf[q] = q < D ? xp[q * ld] : 0.0;
+  for (int q = 0; q < PF; ++q) pf[q] = q < D ? __builtin_nontemporal_load(xp + q * ld) : 0.0;
   xp += PF * ld;
   int64_t off = off0;
   int64_t d0 = 0;
@@ -419,7 +421,7 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
 #pragma unroll
     for (int q = 0; q < W; ++q) {
       const double v = pf[q % PF];
-      pf[q % PF] = *xp;
+      pf[q % PF] = __builtin_nontemporal_load(xp);
       xp += ld;
       ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
       off += ld;
@@ -432,7 +434,7 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
       const int64_t d = d0 + q;
       if (d < D) {
         const double v = pf[q % PF];
-        if (d + PF < D) pf[q % PF] = *xp;
+        if (d + PF < D) pf[q % PF] = __builtin_nontemporal_load(xp);
         xp += ld;
         ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
         off += ld;
@@ -1053,8 +1055,11 @@ extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, d
   for (int k = 0; k < 5; ++k) FMX_ARG(outs[k] != X, "outputs must not alias X");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   if (!present && window == 20 && rank_window == 10 && getenv("FMX_TS_SET_SPLIT") == nullptr) {
-    static const bool v1 = getenv("FMX_TS_SET_V1") != nullptr;    // A/B switch to the IEEE-divide kernel
-    if (!v1 && (D + 40) * ld * (int64_t)sizeof(double) < ((int64_t)1 << 32) && F <= 65535) {
+    // k_ts_set2 (VALU diet) measured slower than k_ts_set at C2 (30.2 vs 28.6 ms,
+    // profiles/r02/kbench_w2_*.log): the set is bound by its 1-read / 5-write HBM stream,
+    // not by VALU.  Kept as an opt-in A/B variant.
+    static const bool v2 = getenv("FMX_TS_SET_V2") != nullptr;
+    if (v2 && (D + 40) * ld * (int64_t)sizeof(double) < ((int64_t)1 << 32) && F <= 65535) {
       k_ts_set2<20, 10, 5><<<dim3((unsigned)ceil_div(A, 256), (unsigned)F), 256, 0, as_stream(stream)>>>(
           X, Ymean, Ystd, Yzscore, Yrank, Ydecay, D, A, ld);
       FMX_LAUNCH_CHECK("k_ts_set2");

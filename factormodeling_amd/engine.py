@@ -149,6 +149,7 @@ def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=Fal
 
 
 RANKED_IC_MAX_A = 16384
+BITONIC_RANK_MAX_A = 8192   # fmx_cs_rank's LDS bitonic path (methods first / dense)
 _WORK = {}
 
 
@@ -209,6 +210,13 @@ def cs_rank(X, method="average", present=None, out=None):
     if method not in RANK:
         raise ValueError(f"unknown rank method {method!r}")
     Y = _out(X, out)
+    if method in ("first", "dense") and A > BITONIC_RANK_MAX_A:
+        # rows past the LDS bitonic kernel: sorted in HBM (fmx_cs_rank_sorted)
+        nb = int(_lib.load().fmx_cs_rank_sorted_work_bytes(F, D, A))
+        work, wb = _workspace_bytes(X.device, nb)
+        call("fmx_cs_rank_sorted", ptr(X), ptr(Y), F, D, A, A, RANK[method], ptr(present), ptr(work), wb,
+             stream_ptr())
+        return Y
     call("fmx_cs_rank", ptr(X), ptr(Y), F, D, A, A, RANK[method], ptr(present), stream_ptr())
     return Y
 

@@ -152,6 +152,13 @@ fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t
 fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
                               int64_t ld, double qlo, double qhi, const uint8_t* present, uint32_t* rank2,
                               void* stream);
+/* cs_rank(method='first' | 'dense') for any row length (A <= 65535): rows sorted in HBM
+ * (rocPRIM segmented radix sort of (value key, asset) pairs, stable), then one workgroup
+ * per row scatters the ranks.  fmx_cs_rank takes these methods up to A = 8192 (LDS
+ * bitonic); this entry has no such limit.  work: fmx_cs_rank_sorted_work_bytes(F, D, A). */
+fmx_status fmx_cs_rank_sorted(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
+                              const uint8_t* present, void* work, int64_t work_bytes, void* stream);
+int64_t fmx_cs_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
 /* Only the doubled average ranks of fmx_cs_rank_winsor (rank2 [F][D][ld] uint32, A <=
  * 16384): the rank pass of a daily IC over raw factors (fmx_ic_daily_ranked) when no
  * operator output of the same rows is wanted (factor_selector.py:36-48's rankdata). */

@@ -222,3 +222,47 @@ def test_ic_ranked_long_rows_vs_oracle(dev):
             ref = OM.daily_stats(X[0, td - L], R[td])
             assert got[m, 0, 0, td] == ref[0]
             np.testing.assert_allclose(got[m, 1:, 0, td], ref[1:], rtol=1e-9, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.parametrize("A", [9, 777, 5000, 10000])
+def test_cs_rank2_matches_rank_winsor_ranks(dev, A):
+    """The ranks-only pass (fmx_cs_rank2, the C5 IC's rank pass) writes exactly the doubled
+    ranks the fused rank+winsor pass writes."""
+    import torch
+    import factormodeling_amd.engine as E
+    X, _ = _ic_case(A + 7, 2, 6, A, 0.0, x_nan=0.05)
+    X[1, 2] = np.nan                           # empty row
+    X[1, 3, 1:] = np.nan                       # single valid value
+    Xt = torch.as_tensor(X, device=dev)
+    ref = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=ref)
+    got = E.cs_rank2(Xt)
+    assert np.array_equal(got.cpu().numpy(), ref.cpu().numpy())
+
+
+def test_ts_set_division_edge_values(dev):
+    """k_ts_set2 replaces the integer divides by reciprocal + fma corrections (div_rn) with
+    an IEEE fallback for zero / tiny / huge / non-finite dividends: bit-identical to the
+    single-op kernels (IEEE divides) on values that exercise every branch."""
+    import torch
+    import factormodeling_amd.engine as E
+    rng = np.random.default_rng(17)
+    F, D, A = 3, 120, 256
+    X = rng.standard_normal((F, D, A))
+    X[0, :, :64] = 0.0                                           # zero sums
+    X[0, :, 64:96] = -0.0                                        # signed zeros
+    X[0, :, 96:128] *= 1e300                                     # huge (sums overflow to inf)
+    X[0, :, 128:160] *= 1e-308                                   # subnormal-range dividends
+    X[1] = np.round(X[1] * 3) / 7.0                              # many exact ties / repeating thirds
+    X[1, 30:50, :32] = np.inf
+    X[1, 60:70, 32:64] = -np.inf
+    X[2] = 1e8 + rng.standard_normal((D, A)) * 1e-4              # large offset, tiny spread
+    X[2, rng.random((D, A)) < 0.05] = np.nan
+    Xt = torch.as_tensor(X, device=dev)
+    outs = {k: torch.empty_like(Xt) for k in E.TS_SET}
+    E.ts_set(Xt, outs, 20, 10)
+    for k in E.TS_SET:
+        ref = E.ts(k, Xt, 10 if k == "rank" else 20).cpu().numpy()
+        got = outs[k].cpu().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(ref)), k
+        assert np.array_equal(got.view(np.uint64)[~np.isnan(got)], ref.view(np.uint64)[~np.isnan(ref)]), k

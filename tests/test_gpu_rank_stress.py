@@ -71,6 +71,46 @@ def test_cs_rank_stress(eng, A):
 
 
 @pytest.mark.parametrize("A", SIZES)
+def test_cs_rank_first_dense_stress(eng, A):
+    """Methods 'first' / 'dense': LDS bitonic up to A = 8192, rows sorted in HBM beyond
+    (fmx_cs_rank_sorted); bit-exact vs the oracle, incl. a ragged presence mask."""
+    import oracle.ops as O
+    E, torch = eng
+    x = adversarial_rows(A, A + 3)
+    Xd = torch.as_tensor(x[None], device="cuda")
+    pres = (np.random.default_rng(A).random(x.shape) > 0.15).astype(np.uint8)
+    pres[8] = 0
+    pres[8, A // 2] = 1                                              # single-row date
+    Pd = torch.as_tensor(pres, device="cuda")
+    for method in ("first", "dense"):
+        got = E.cs_rank(Xd, method=method).cpu().numpy()[0]
+        ref = O.cs_rank(x, method=method)
+        assert_close(got.ravel(), ref.ravel(), exact=True, what=f"cs_rank[{method}] A={A}")
+        got = E.cs_rank(Xd, method=method, present=Pd).cpu().numpy()[0]
+        ref = O.cs_rank(x, present=pres.astype(bool), method=method)
+        assert_close(got.ravel(), ref.ravel(), exact=True, what=f"cs_rank[{method}] ragged A={A}")
+
+
+def test_cs_rank_sorted_equals_bitonic(eng):
+    """The HBM-sorted path equals the LDS bitonic path where both run (A <= 8192)."""
+    import ctypes
+    from factormodeling_amd import _lib
+    E, torch = eng
+    A = 5000
+    X = torch.as_tensor(adversarial_rows(A, 9)[None].repeat(3, axis=0), device="cuda")
+    F, D = X.shape[0], X.shape[1]
+    for method in ("first", "dense"):
+        ref = E.cs_rank(X, method=method)
+        Y = torch.empty_like(X)
+        nb = int(_lib.load().fmx_cs_rank_sorted_work_bytes(F, D, A))
+        work = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        _lib.call("fmx_cs_rank_sorted", ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(Y.data_ptr()), F, D, A, A,
+                  E.RANK[method], None, ctypes.c_void_p(work.data_ptr()), nb,
+                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert np.array_equal(Y.cpu().numpy(), ref.cpu().numpy(), equal_nan=True), method
+
+
+@pytest.mark.parametrize("A", SIZES)
 def test_cs_quantile_stress(eng, A):
     import oracle.ops as O
     E, torch = eng

@@ -4,7 +4,7 @@
 # pass over the wide Gram (kbench, C4 factors/assets on 252 dates).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 T=${1:-r2}
-KOPS="ts_mean,ts_set,cs_zn,cs_rw,ic,gram"
+KOPS="ts_mean,ts_set,cs_zn,cs_rw_rk,ic_ranked,gram"
 trap 'find gpurun_out -name "*kernel_trace.csv" -size +2M -delete; find gpurun_out -name "*agent_info.csv" -delete' EXIT
 tools/gpu_run.sh \
  "prof_c2_$T:300:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_c2_$T -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline" \
