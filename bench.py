@@ -62,7 +62,7 @@ def bytes_per_unit(stage, F, ranked=False):
 
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
-STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave(", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
+STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
                 "ts_set": ("fmx::k_ts_set2<", "fmx::k_ts_set<"), "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
@@ -82,8 +82,8 @@ def pmc_traffic(stage, dims):
         return None
     if list(t.get("dims", [])) != list(dims):
         return None
-    key = ":".join(stage.split(":")[:2]).rstrip(":")
-    pre = STAGE_KERNEL.get(key)
+    parts = stage.split(":")
+    pre = STAGE_KERNEL.get(":".join(parts[:2]).rstrip(":")) or STAGE_KERNEL.get(parts[0])
     for name, v in t.get("kernels", {}).items():
         if pre and name.startswith(pre if isinstance(pre, tuple) else (pre,)):
             return v["traffic_bytes"]

@@ -51,8 +51,9 @@ __device__ __forceinline__ double okey_inv(uint64_t k) {
 }
 constexpr uint64_t KEY_SENTINEL = 0xffffffffffffffffull;  // sorts after +inf
 
-// a / b, bit-identical to the IEEE quotient, for b >= 1 given y = RN(1 / b) (a reciprocal
-// table or a compile-time constant).  q0 = RN(a y) is within 1.5 ulp of a / b; one fma
+// a / b, bit-identical to the IEEE quotient, for b > 0 normal with y = RN(1 / b) normal
+// (a reciprocal table, a per-row reciprocal or a compile-time constant) and a quotient in
+// the normal range.  q0 = RN(a y) is within 1.5 ulp of a / b; one fma
 // correction (exact remainder e = a - q b) makes it faithful, and a second one rounds
 // correctly (Markstein's theorem: y the correctly rounded reciprocal, q faithful).  Zero,
 // very small, infinite and NaN dividends take the IEEE division instead (a branch that

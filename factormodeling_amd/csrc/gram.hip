@@ -439,11 +439,11 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
 // waves' MFMAs), issues the loads of chunk c+2, runs chunk c's MFMAs, then one barrier.
 // Slices are equal ranges of the flattened (date, 32-asset block) chunk sequence, one per
 // CU.  The row stats are double-buffered by date parity, loaded one date ahead.
-template <int NB>
+template <int NB, int EXP = 0>   // EXP: timing experiments (1 no LDS fragment reads, 2 no staging)
 __global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
           int64_t ld, int64_t d0, int64_t nch, int64_t total, int64_t nslice, double* __restrict__ part,
-          uint32_t* __restrict__ mbits) {
+          uint32_t* __restrict__ mbits, int opt) {
   constexpr int FP = 16 * NB;
   constexpr int NTRI = NB * (NB + 1) / 2;
   constexpr int NWV = SG_NT / 64;
@@ -451,7 +451,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   constexpr int NEL = FP * SG_K;
   constexpr int EPT = (NEL + SG_NT - 1) / SG_NT;
   __shared__ double Zs[2][FP * SG_KP];
-  __shared__ double mu_s[2][FP], sd_s[2][FP];
+  __shared__ double mu_s[2][FP], sd_s[2][FP], rs_s[2][FP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t slice = blockIdx.x;
   const int64_t c0 = slice * total / nslice, c1 = (slice + 1) * total / nslice;
@@ -485,11 +485,15 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
     const int p = (int)(dr & 1);
     for (int r = tid; r < FP; r += SG_NT) {
       mu_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr)] : 0.0;
-      sd_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
+      const double sd = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
+      sd_s[p][r] = sd;
+      const double rs = 1.0 / sd;                 // RN(1 / sd) for div_rn (0: IEEE divide)
+      rs_s[p][r] = (sd >= 0x1p-900 && rs >= 0x1p-900 && rs <= 0x1p+900) ? rs : 0.0;
     }
   };
   // stage the chunk held in xr (global chunk index c, date dr) into buffer b
   auto stage = [&](int64_t c, int64_t dr, int b) {
+    if (EXP & 2) return;
     const int p = (int)(dr & 1);
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
@@ -497,7 +501,11 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
       if (e >= NEL) continue;                     // wave-uniform (NEL is a multiple of 64)
       const double v = xr[u], sd = sd_s[p][r];
       const bool ok = (v == v) && (sd > 0.0);
-      Zs[b][r * SG_KP + cl] = ok ? (v - mu_s[p][r]) / sd : 0.0;
+      // (v - mu) / sd bit-identically via the row's reciprocal (div_rn); sd is a normal
+      // positive number wherever ok (the row stats of a non-constant row)
+      const double rs = rs_s[p][r];
+      Zs[b][r * SG_KP + cl] =
+          ok ? ((opt & 1) && rs > 0.0 ? div_rn(v - mu_s[p][r], sd, rs) : (v - mu_s[p][r]) / sd) : 0.0;
       const uint64_t bal = __ballot(ok);
       if ((lane & 31) == 0 && r < F) mbits[(uint32_t)c * (uint32_t)F + (uint32_t)r] = (uint32_t)(bal >> lane);
     }
@@ -513,28 +521,37 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   stage(c0, cur_d, 0);
   if (c0 + 1 < c1) issue();
   __syncthreads();
+  // half the waves of each SIMD (waves s, s+4, s+8, s+12 share SIMD s) run their MFMAs
+  // before staging the next chunk and half after, so the SIMD's MFMA pipe is not idle
+  // while all four waves do the staging VALU work at the same time
+  const bool mfma_first = (opt & 2) && ((wid >> 2) & 1);
   for (int64_t c = c0; c < c1; ++c) {
     const int b = (int)((c - c0) & 1);
-    if (c + 1 < c1) {
-      const int64_t dn = (c + 1) / nch;           // date of chunk c + 1
-      stage(c + 1, dn, b ^ 1);                    // its stats were loaded a date ahead
-      if (c + 2 < c1) {
-        if ((c + 2) % nch == 0) load_stats(dn + 1);   // the buffer of date dn - 1: dead
-        issue();
+    auto next = [&]() {
+      if (c + 1 < c1) {
+        const int64_t dn = (c + 1) / nch;         // date of chunk c + 1
+        stage(c + 1, dn, b ^ 1);                  // its stats were loaded a date ahead
+        if (c + 2 < c1) {
+          if ((c + 2) % nch == 0) load_stats(dn + 1);   // the buffer of date dn - 1: dead
+          issue();
+        }
       }
-    }
+    };
+    if (!mfma_first) next();
 #pragma unroll 1
     for (int ks = 0; ks < SG_K; ks += 4) {
       const int kk = ks + (lane >> 4);
+      const double a0 = (EXP & 1) ? Zs[b][(lane & 15) * SG_KP + kk] : 0.0;
 #pragma unroll
       for (int u = 0; u < BPW; ++u) {
         if (blk[u] < 0) continue;                 // wave-uniform
         const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
-        const double a = Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
-        const double bb = Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
+        const double a = (EXP & 1) ? a0 : Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
+        const double bb = (EXP & 1) ? a0 : Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
         gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
       }
     }
+    if (mfma_first) next();
     __syncthreads();
   }
   double* p = part + slice * (int64_t)FP * FP;
@@ -674,7 +691,17 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   static const bool db = getenv("FMX_GRAM_SINGLE_BUFFER") == nullptr;   // A/B switch
   if (!mask_mfma && db) {
     const int64_t nch = ceil_div(A, (int64_t)SG_K);
-    k_gram_db<NB><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits);
+    static const int exp = getenv("FMX_GRAM_EXP") ? atoi(getenv("FMX_GRAM_EXP")) : 0;   // timing only
+    // bit 0: z-score by div_rn with the row reciprocal, bit 1: MFMA / staging interleave
+    static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
+    if (NB == 13 && exp == 1)
+      k_gram_db<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
+    else if (NB == 13 && exp == 2)
+      k_gram_db<NB, 2><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
+    else if (NB == 13 && exp == 3)
+      k_gram_db<NB, 3><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
+    else
+      k_gram_db<NB><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
     FMX_LAUNCH_CHECK("k_gram_db");
   } else {
     const int64_t dps2 = mask_mfma ? dps : ceil_div(d1 - d0, nslice);

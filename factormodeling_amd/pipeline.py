@@ -230,6 +230,11 @@ class EngineBackend:
 
     ranked_ic_max_a = E.RANKED_IC_MAX_A
 
+    # the ranks-only pass stages a row's keys in LDS (8 B per asset): past ~6k assets a CU
+    # holds one row, and rank pass + wave IC (C5, 10,000 assets: 420 + 76 ms) loses to the
+    # standalone IC kernel (227 ms), profiles/r02/c5_h1.log
+    rank_pass_max_a = 6144
+
     @staticmethod
     def cs_rank2(X, rank2):
         """The doubled ranks alone (no operator output): the IC's rank pass."""
@@ -376,7 +381,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
     if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
-            and sp.A <= be.ranked_ic_max_a):
+            and sp.A <= getattr(be, "rank_pass_max_a", 0)):
         # no operator ranked X this step: one ranks-only pass feeds the wave IC
         t0 = _ev(timers)
         rk = getattr(sp, "rank2", None)

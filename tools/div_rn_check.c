@@ -28,12 +28,14 @@ int main(){
   double bs[80]; int nb=0;
   for(int k=1;k<=64;k++) bs[nb++]=k;
   bs[nb++]=210; bs[nb++]=55; bs[nb++]=1830; bs[nb++]=3;
+  /* non-integer divisors (row standard deviations): random significands, exponents +-40 */
+  for(int k=0;k<8;k++){ uint64_t r=xr(); bs[nb++]=bits(((uint64_t)(1023-40+(r%80))<<52)|(xr()&((1ull<<52)-1))); }
   for(int bi=0;bi<nb;bi++){
     double b=bs[bi], y=1.0/b;
     for(long i=0;i<5000000;i++){
       uint64_t r=xr();
       // exponents in a moderate range [-900, 900], random mantissa, random sign
-      uint64_t e=(uint64_t)(1023-900+(r%1800));
+      uint64_t e=(uint64_t)(1023-850+(r%1700));
       uint64_t m=xr()&((1ull<<52)-1);
       if(i%4==0) m = (m & ~((1ull<<40)-1)); // fewer mantissa bits (decimal-ish)
       if(i%8==1) m = (1ull<<52)-1-(m&0xff);
