@@ -726,7 +726,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
 // ic_ranked_row: one 1024-thread workgroup per row, any E_m -- the rows the wave kernel
 // (k_ic_wave, below) hands over.  E_m keys gathered in LDS while the row loads, sorted by
 // one wave when < 64 (a sentinel ends the list) and binary-searched; a longer E_m is
-// gathered register-chunk by chunk and scanned.  Sums and two-pass moments as in
+// counting-sorted by 64-rank blocks of the members' doubled ranks (O(A + |E|)).  Sums and two-pass moments as in
 // k_ic_daily_fr (same element order, same butterflies: the records are bit-identical).
 template <int NT, int EMAX>
 __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restrict__ X,
@@ -736,7 +736,8 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
   constexpr int NW = NT / 64, ES = 64;
   __shared__ double dscr[(NW + 1) * 16];
   __shared__ uint64_t el[2][ES];              // E_m keys (first ES), then sorted
-  __shared__ uint64_t tb[NT];                 // long E_m: one register chunk's keys
+  __shared__ uint32_t ltbl[(2 * 16384 >> 6) + 2];   // long E_m: 64-rank block table (A <= 16384)
+  __shared__ uint32_t lent[16384];                 //            entries grouped by block
   __shared__ int ecnt[2], wcnt[NW];
   __shared__ double cst[8], fin[16];
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
@@ -852,42 +853,46 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
         cr[k] -= (uint32_t)(lo + le) << (16 * m);
       }
     }
+    // long E_m (any size): counting-sort the E members' doubled ranks into 64-rank blocks
+    // (key order = rank order within the row) -- the same table as k_ic_wave, so each pair
+    // element's correction is 2 * #entries of earlier blocks + a scan of its own block's
+    // (few) entries: O(A + |E|) per row instead of O(A * |E|)
+    const int nb = (int)((2 * A) >> 6) + 1;
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      if (ne[m] < ES) continue;
-      // long E_m: gather register chunk c's E members in asset order, scan them
-#pragma unroll 1
-      for (int c = 0; c < EMAX; ++c) {
-        const bool ex = (em >> (2 * c + m)) & 1;
-        const uint64_t b = __ballot(ex);
-        if (lane == 0) wcnt[wid] = __popcll(b);
-        __syncthreads();
-        int off = 0, tot_c = 0;
+      if (ne[m] < ES) continue;               // block-uniform
+      for (int b = t; b < nb; b += NT) ltbl[b] = 0u;
+      __syncthreads();
+      int sl[EMAX];
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const int cw = wcnt[w];
-          off += w < wid ? cw : 0;
-          tot_c += cw;
-        }
-        if (ex) {
-          double xc = xv[0];
-#pragma unroll
-          for (int k = 1; k < EMAX; ++k) xc = c == k ? xv[k] : xc;
-          tb[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = okey(xc);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < EMAX; ++k) {
-          if (!((pm >> (2 * k + m)) & 1)) continue;
-          const uint64_t key = okey(xv[k]);
-          uint32_t a = 0;
-          for (int j = 0; j < tot_c; ++j) {
-            const uint64_t w = tb[j];
-            a += (w < key ? 1u : 0u) + (w <= key ? 1u : 0u);
-          }
-          cr[k] -= a << (16 * m);
-        }
+      for (int k = 0; k < EMAX; ++k)
+        sl[k] = ((em >> (2 * k + m)) & 1) ? (int)atomicAdd(&ltbl[rk[k] >> 6], 1u) : 0;
+      __syncthreads();
+      {
+        // exclusive scan of the block counts, NT >= nb (A <= 16384 -> nb <= 513)
+        const int n = t < nb ? (int)ltbl[t] : 0;
+        int tot;
+        const int st0 = block_exscan<NT>(n, wcnt, &tot);
+        if (t < nb) ltbl[t] = (uint32_t)st0 | ((uint32_t)(st0 + n) << 16);
       }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k)
+        if ((em >> (2 * k + m)) & 1) lent[(ltbl[rk[k] >> 6] & 0xffffu) + sl[k]] = rk[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        if (!((pm >> (2 * k + m)) & 1)) continue;
+        const uint32_t tb2 = ltbl[rk[k] >> 6];
+        const uint32_t j0 = tb2 & 0xffffu, j1 = tb2 >> 16;
+        uint32_t a = 2u * j0;
+        for (uint32_t j = j0; j < j1; ++j) {
+          const uint32_t e = lent[j];
+          a += (e < rk[k] ? 1u : 0u) + (e <= rk[k] ? 1u : 0u);
+        }
+        cr[k] -= a << (16 * m);
+      }
+      __syncthreads();                        // the table is reused by the next lag
     }
     BR_PH();
     double fm[2], rm[2], km[2];

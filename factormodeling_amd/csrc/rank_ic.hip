@@ -77,12 +77,13 @@ k_nan_positions(const double* __restrict__ Rt, int64_t D, int64_t A, int64_t ld,
 // ------------------------------------------------------------------------------------
 // Daily IC from the ranks, one WAVE per row: no workgroup barrier anywhere, so ~20 rows
 // are in flight per CU instead of two 1024-thread rows.
-//  1. E_m from the target date's NaN-return positions: gather x there (< 64 valid, else
-//     the row goes to the overflow list for ic_ranked_row), wave-sort in LDS.
+//  1. E_m from the target date's NaN-return positions (<= ICW_PC of them, else the row
+//     goes to the overflow list for ic_ranked_row): the doubled ranks of the valid
+//     exposures there, counting-sorted into 64-rank blocks in LDS.
 //  2. one streaming pass over x, RK and the two return rows: per lag, the pair count
 //     (ballots) and sums shifted by the lag's first pair (single-pass moments without
 //     cancellation; constant inputs = nothing differs from that pair); the pair rank is
-//     RK minus a binary search over sorted E_m.
+//     RK minus the E correction read off the rank-block table.
 //  3. multi-value DPP butterflies, lane 0 writes the records.
 // Moments are single-pass about the first pair (rank moments from exact integer sums), so
 // records agree with the two-pass kernels to ~1e-15 relative, not bitwise.
@@ -90,16 +91,7 @@ constexpr int ICW_WAVES = 4;
 #ifndef ICW_UNROLL
 #define ICW_UNROLL 1
 #endif
-__device__ __forceinline__ int icw_search(const uint64_t* e, uint64_t key) {
-  // #keys < key plus #keys <= key in the sorted, sentinel-terminated list of < 64 keys
-  int lo = 0, le = 0;
-#pragma unroll
-  for (int st = 32; st > 0; st >>= 1) {
-    lo += e[lo + st - 1] < key ? st : 0;
-    le += e[le + st - 1] <= key ? st : 0;
-  }
-  return lo + le;
-}
+constexpr int ICW_EC = 256;   // E entries per (wave, lag); more NaN returns: ICW_PC overflow
 
 #ifndef ICW_MINW
 #define ICW_MINW 6
@@ -108,7 +100,10 @@ __global__ void __launch_bounds__(64 * ICW_WAVES, ICW_MINW)
 k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt, int64_t F,
           int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
           const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
-  __shared__ uint64_t el[ICW_WAVES][2][64];
+  // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64);
+  // T[b] = start | end << 16 of its E entries in eb) and the entries eb[ICW_EC] grouped by
+  // block.  Dynamic LDS: ICW_WAVES * 2 * (nbp + ICW_EC) words.
+  extern __shared__ uint32_t icw_lds[];
   __shared__ double scr[ICW_WAVES * 32];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * ICW_WAVES + wid;
@@ -125,10 +120,31 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
   if (!act[0] && !act[1]) return;
   const double* xf = X + (f * D + s) * ld;
   const uint32_t* rkf = RK + (f * D + s) * ld;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  // 1. E lists
+  const int nb = (int)((2 * A) >> 6) + 1;     // doubled ranks are <= 2A
+  const int nbp = (nb + 1) & ~1;
+  uint32_t* T[2];
+  uint32_t* eb[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    T[m] = icw_lds + (wid * 2 + m) * (nbp + ICW_EC);
+    eb[m] = T[m] + nbp;
+  }
+  // 1. E lists: the doubled ranks of the valid exposures at the target date's NaN-return
+  // positions (key(e) < key(x) <=> RK(e) < RK(x), ties alike, so the corrections can be
+  // counted on ranks), counting-sorted by rank block: per element the correction is then
+  // 2 * (#entries of earlier blocks) + one (usually empty) scan of its own block's entries,
+  // one LDS read instead of a binary search (the searches were LDS-bound: 2 lags x 7 reads).
   int ne[2] = {0, 0};
   bool over = false;
+  uint32_t er[2][ICW_EC / 64];                // this lane's entries (0: none) and their slots
+  int es[2][ICW_EC / 64];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    for (int b = lane; b < nbp; b += 64) T[m][b] = 0u;
+#pragma unroll
+    for (int q = 0; q < ICW_EC / 64; ++q) { er[m][q] = 0u; es[m][q] = 0; }
+  }
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     if (!act[m]) continue;
@@ -136,20 +152,18 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
     const int c = npos[td];
     if (c > ICW_PC) { over = true; continue; }
     int k = 0;
-    for (int b = 0; b < c; b += 64) {
-      const int j = b + lane;
-      double v = qnan();
-      if (j < c) v = xf[pos[td * ICW_PC + j]];
-      const bool e = v == v;
-      const uint64_t bal = __ballot(e);
-      const int at = k + __popcll(bal & lt);
-      if (e && at < 64) el[wid][m][at] = okey(v);
-      k += __popcll(bal);
+#pragma unroll
+    for (int q = 0; q < ICW_EC / 64; ++q) {
+      const int j = 64 * q + lane;
+      if (64 * q >= c) break;                 // wave-uniform
+      const uint32_t r2 = j < c ? rkf[pos[td * ICW_PC + j]] : 0u;   // 0: NaN exposure
+      er[m][q] = r2;
+      if (r2) es[m][q] = (int)atomicAdd(&T[m][r2 >> 6], 1u);
+      k += __popcll(__ballot(r2 != 0u));
     }
-    if (k >= 64) over = true;
     ne[m] = k;
   }
-  if (over) {                                 // a long E list: the workgroup kernel takes the row
+  if (over) {                                 // > ICW_PC NaN returns: the workgroup kernel takes the row
     if (lane == 0) {
       const int q = atomicAdd(&ovf[0], 1);
       ovf[1 + q] = (int32_t)row;
@@ -159,11 +173,35 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    if (ne[m] == 0) continue;
-    const uint64_t v = lane < ne[m] ? el[wid][m][lane] : KEY_SENTINEL;
+    if (ne[m] == 0) continue;                 // wave-uniform
+    // exclusive scan of the block counts: lane l owns blocks [l R, l R + R)
+    const int R = (nbp + 63) >> 6;
+    int loc = 0;
+    for (int q = 0; q < R; ++q) {
+      const int b = lane * R + q;
+      loc += b < nbp ? (int)T[m][b] : 0;
+    }
+    int incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = fr_up(incl, o, lane);
+      if (lane >= o) incl += u;
+    }
+    int run = incl - loc;
+    for (int q = 0; q < R; ++q) {
+      const int b = lane * R + q;
+      if (b < nbp) {
+        const int n = (int)T[m][b];
+        T[m][b] = (uint32_t)run | ((uint32_t)(run + n) << 16);
+        run += n;
+      }
+    }
     __builtin_amdgcn_wave_barrier();
-    el[wid][m][lane] = wave_sort64(v, lane);
+#pragma unroll
+    for (int q = 0; q < ICW_EC / 64; ++q)
+      if (er[m][q]) eb[m][(T[m][er[m][q] >> 6] & 0xffffu) + es[m][q]] = er[m][q];
   }
+  __builtin_amdgcn_wave_barrier();
   // 2. one pass.  Per lag: pair count (ballots); the first pair's (x, r) is the lag's
   // shift (a, b) and reference (constant inputs: no pair differs from it); sums of x', r',
   // x'^2, r'^2, x'r' (x' = x - a, r' = r - b), of 2k * r' and (2k)^2 (exact integers) with
@@ -188,7 +226,6 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
     double r[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) r[m] = (in && act[m]) ? rr[m][i] : qnan();
-    const uint64_t key = okey(x);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const bool p = x == x && r[m] == r[m];
@@ -202,7 +239,16 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
         ref[m] = true;
       }
       if (!p) continue;
-      const int corr = ne[m] ? icw_search(el[wid][m], key) : 0;
+      int corr = 0;
+      if (ne[m]) {
+        const uint32_t tb = T[m][rk >> 6];
+        const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16;
+        corr = 2 * (int)j0;
+        for (uint32_t j = j0; j < j1; ++j) {  // this block's entries (usually none)
+          const uint32_t e = eb[m][j];
+          corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
+        }
+      }
       const uint32_t k2 = rk - (uint32_t)corr;
       const double dx = x - ax[m], dy = r[m] - ar[m];
       dif |= ((x != ax[m]) ? 1u : 0u) << (2 * m);
@@ -299,7 +345,9 @@ fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, in
     k_ic_empty<<<(unsigned)F, 64, 0, st>>>(o, F, D, L0, L1, NL);
     FMX_LAUNCH_CHECK("k_ic_empty");
     FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
-    k_ic_wave<<<wave_grid, 64 * ICW_WAVES, 0, st>>>(X, RK, R, F, D, A, ld, L0, L1, NL, o, pos, npos, ovf);
+    const int nbp = ((int)((2 * A) >> 6) + 2) & ~1;
+    const size_t lds = sizeof(uint32_t) * ICW_WAVES * 2 * (size_t)(nbp + ICW_EC);
+    k_ic_wave<<<wave_grid, 64 * ICW_WAVES, lds, st>>>(X, RK, R, F, D, A, ld, L0, L1, NL, o, pos, npos, ovf);
     FMX_LAUNCH_CHECK("k_ic_wave");
     void* args[] = {(void*)&X, (void*)&RK, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,
                     (void*)&L1, (void*)&NL, (void*)&o, (void*)&ovf};

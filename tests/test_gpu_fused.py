@@ -127,8 +127,9 @@ def _ic_case(seed, F, D, A, r_nan, x_nan=0.02):
     return X, R
 
 
-@pytest.mark.parametrize("A,r_nan", [(9, 0.1), (300, 0.005), (1000, 0.05), (5000, 0.005), (5000, 0.03),
-                                     (10000, 0.005), (12000, 0.002)])
+@pytest.mark.parametrize("A,r_nan", [(9, 0.1), (300, 0.005), (1000, 0.05), (5000, 0.005), (5000, 0.02),
+                                     (5000, 0.03), (5000, 0.045), (10000, 0.005), (12000, 0.002),
+                                     (12000, 0.015)])
 @pytest.mark.parametrize("lags", [(1, 2), (1,), (0, 2, 5)])
 def test_ic_ranked_matches_standalone_ic(dev, A, r_nan, lags):
     """Daily IC from cs_rank_winsor's doubled ranks (one wave per row, single-pass shifted

@@ -46,7 +46,7 @@ def panel(D, A, F, seed=0, block=8):
     x = np.where(u < 0.05, np.round(x, 1), x)
     x[u > 0.99] = np.nan
     r = 0.01 * rng.standard_normal((D, A))
-    r[rng.random((D, A)) < 0.005] = np.nan
+    r[rng.random((D, A)) < float(os.environ.get("KB_R_NAN", "0.005"))] = np.nan
     Xb = torch.as_tensor(x, device="cuda")
     reps = (F + fb - 1) // fb
     X = Xb.repeat(reps, 1, 1)[:F].contiguous()
