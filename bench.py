@@ -257,6 +257,8 @@ def main():
     A = args.assets or dims[1]
     F = args.factors or dims[2]
     cfg = PL.workload_config(args.workload)
+    if os.environ.get("FMX_STEP_STREAMS") == "1":
+        cfg.streams = True                      # A/B: the step's independent chains on 3 streams
     sp = PL.ShardedPanel(D, A, F, rank, world, dev, seed=0, halo=cfg.halo)
     torch.cuda.synchronize()
 
@@ -325,7 +327,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SURVEY 8(d) generator, device-generated)",
             "config": {"workload": WORKLOAD_NAME[args.workload], "dates": D, "assets": A, "factors": F,
-                       "parallelism": f"date-shard{world}", "sel_window": cfg.sel_window, "top_x": cfg.top_x},
+                       "parallelism": f"date-shard{world}", "sel_window": cfg.sel_window, "top_x": cfg.top_x,
+                       "streams": 3 if (cfg.streams and cfg.ops) else 1},
             "roofline": roofline,
             "stages_ms": {k: round(v / args.steps, 3) for k, v in stages.items()},
             "step_bytes_per_unit": step_bpu,

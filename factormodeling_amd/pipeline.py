@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -53,6 +55,10 @@ class StepConfig:
     composite: object = None   # "zscore" | "rank": weighted composite of the day's selection
     names: object = None       # factor names (composite suffix / prefix rules)
     rank_pass: bool = False    # no op stage ranks X: rank it once (cs_rank2) for the daily IC
+    # independent chains on their own HIP streams (engine backend).  Off by default: at C2
+    # the overlap gains 2.5 % (87.5 vs 89.7 ms/step) while every stage runs 1.4-3x longer
+    # under contention (profiles/r02/streams_ab.log)
+    streams: bool = False
 
     @property
     def lookback(self):
@@ -281,48 +287,76 @@ class EngineBackend:
 ENGINE = EngineBackend()
 
 
-def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None):
+def _stage_stream(name, streams):
+    """The stream a planned stage runs on (None: the current stream).  Three independent
+    chains of the step: the rolling set (streams[0]); cs_zscore + market_neutralize, whose
+    row stats feed the Gram (streams[1]); the rank pass, whose ranks feed the daily IC
+    (current stream)."""
+    if not streams:
+        return None
+    if name.startswith("ts_set:"):
+        return streams[0]
+    if name == "cs_zscore_neutralize":
+        return streams[1]
+    return None
+
+
+def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None,
+            streams=None):
     """Operator set over the local panel (halo rows included as warm-up), as planned by
     ``plan_ops``; every operator writes its own output buffer (``bufs``: a list of tensors
-    shaped like X, reused across steps; as many as the widest fused launch).  ``collect``
-    (a dict) receives a copy of every operator's owned-date output (tests only); ``side``
-    (a dict) receives by-products later stages reuse (cs_zscore's row stats; "rank2", the
-    doubled ranks of X, written into side["rank2_buf"] when it fits)."""
+    shaped like X, reused across steps).  Sequentially, stages share the buffers (as many
+    as the widest fused launch); with ``streams`` (stages running concurrently) every
+    stage gets its own.  ``collect`` (a dict) receives a copy of every operator's
+    owned-date output (tests only); ``side`` (a dict) receives by-products later stages
+    reuse (cs_zscore's row stats; "rank2", the doubled ranks of X, written into
+    side["rank2_buf"] when it fits)."""
     stages = plan_ops(cfg.ops, be, cfg.fuse)
-    need = max(len(o) for _, o in stages)
+    offs, need = [], 0
+    for _, ops in stages:
+        offs.append(need if streams else 0)
+        need = need + len(ops) if streams else max(need, len(ops))
     bufs = list(bufs or [])
     while len(bufs) < need:
         bufs.append(torch.empty_like(X))
-    for name, ops in stages:
-        outs = bufs[:len(ops)]
-        t0 = _ev(timers)
-        if name.startswith("ts_set:"):
-            be.ts_set(X, ops, outs)
-        elif name == "cs_zscore_neutralize":
-            st = be.cs_zscore_neutralize(X, outs)
-            if side is not None:
-                side["stats"] = st
-        elif name == "cs_rank_winsor":
-            if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
-                # the ranks of X also feed the daily IC (no second ranking of the panel)
-                rk = side.get("rank2_buf")
-                if rk is None or tuple(rk.shape) != tuple(X.shape):
-                    rk = torch.empty(X.shape, dtype=torch.int32, device=X.device)
-                side["rank2"] = rk
-                be.cs_rank_winsor(X, outs, rank2=rk)
-            else:
-                be.cs_rank_winsor(X, outs)
-        else:
-            kind, op, w = ops[0]
-            if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
-                _, side["stats"] = be.cs_zscore_stats(X, outs[0])
-            else:
-                be.op(kind, op, w, X, outs[0])
-        _rec(timers, name, t0)
-        if collect is not None:
-            for o, y in zip(ops, outs):
-                collect[_op_key(*o)] = y[:, own].clone()
+    for (name, ops), off in zip(stages, offs):
+        outs = bufs[off:off + len(ops)]
+        st = _stage_stream(name, streams)
+        ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
+        with ctx:
+            _run_stage(name, ops, outs, X, be, side, timers, collect, own)
     return bufs
+
+
+def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
+    """One planned stage (fused or single operator) on the current stream."""
+    t0 = _ev(timers)
+    if name.startswith("ts_set:"):
+        be.ts_set(X, ops, outs)
+    elif name == "cs_zscore_neutralize":
+        st = be.cs_zscore_neutralize(X, outs)
+        if side is not None:
+            side["stats"] = st
+    elif name == "cs_rank_winsor":
+        if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
+            # the ranks of X also feed the daily IC (no second ranking of the panel)
+            rk = side.get("rank2_buf")
+            if rk is None or tuple(rk.shape) != tuple(X.shape):
+                rk = torch.empty(X.shape, dtype=torch.int32, device=X.device)
+            side["rank2"] = rk
+            be.cs_rank_winsor(X, outs, rank2=rk)
+        else:
+            be.cs_rank_winsor(X, outs)
+    else:
+        kind, op, w = ops[0]
+        if side is not None and (kind, op) == ("cs", "zscore") and hasattr(be, "cs_zscore_stats"):
+            _, side["stats"] = be.cs_zscore_stats(X, outs[0])
+        else:
+            be.op(kind, op, w, X, outs[0])
+    _rec(timers, name, t0)
+    if collect is not None:
+        for o, y in zip(ops, outs):
+            collect[_op_key(*o)] = y[:, own].clone()
 
 
 def _ev(timers):
@@ -375,9 +409,25 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     sp.exchange_halo()
     _rec(timers, "halo", t0)
     side = {"rank2_buf": getattr(sp, "rank2", None)}   # filled as "rank2" when this step ranks X
+    streams = None
+    if cfg.streams and cfg.ops and hasattr(be, "ts_set") and sp.X.is_cuda:
+        # fork: the rolling set and the cs_zscore -> Gram chain on side streams, the rank
+        # pass -> IC -> selection chain on the current one; joined before the Gram sum
+        streams = getattr(sp, "streams", None)
+        if streams is None:
+            streams = sp.streams = [torch.cuda.Stream(sp.X.device) for _ in range(2)]
+        main = torch.cuda.current_stream(sp.X.device)
+        for st in streams:
+            st.wait_stream(main)
     if cfg.ops:
         sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                          own=slice(sp.halo, None), side=side)
+                          own=slice(sp.halo, None), side=side, streams=streams)
+    GN = None
+    if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
+        with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
+            t0 = _ev(timers)
+            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
+            _rec(timers, "gram", t0)
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
     if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
@@ -426,11 +476,19 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         t0 = _ev(timers)
         comp = weighted_composite_step(sp, cfg, w, be)
         _rec(timers, "composite", t0)
+    if streams is not None:                       # join
+        main = torch.cuda.current_stream(sp.X.device)
+        for st in streams:
+            main.wait_stream(st)
     kept = C = None
     if cfg.gram:
         # correlation Gram over owned dates, summed over ranks in rank order
         t0 = _ev(timers)
-        if hasattr(be, "corr_gram"):
+        if GN is not None:
+            G, N = GN                             # made on streams[1]: now used on this one
+            G.record_stream(torch.cuda.current_stream(G.device))
+            N.record_stream(torch.cuda.current_stream(N.device))
+        elif hasattr(be, "corr_gram"):
             G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
         else:
             Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
@@ -438,7 +496,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         if sp.world > 1:
             G, N = ordered_sum(G, sp.world), ordered_sum(N, sp.world)
         C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
-        _rec(timers, "gram", t0)
+        _rec(timers, "gram_sum" if GN is not None else "gram", t0)
         t0 = _ev(timers)
         rir = summ[0, :, 3]
         full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)
