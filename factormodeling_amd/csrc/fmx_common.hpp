@@ -51,26 +51,6 @@ __device__ __forceinline__ double okey_inv(uint64_t k) {
 }
 constexpr uint64_t KEY_SENTINEL = 0xffffffffffffffffull;  // sorts after +inf
 
-// a / b, bit-identical to the IEEE quotient, for b > 0 normal with y = RN(1 / b) normal
-// (a reciprocal table, a per-row reciprocal or a compile-time constant) and a quotient in
-// the normal range.  q0 = RN(a y) is within 1.5 ulp of a / b; one fma
-// correction (exact remainder e = a - q b) makes it faithful, and a second one rounds
-// correctly (Markstein's theorem: y the correctly rounded reciprocal, q faithful).  Zero,
-// very small, infinite and NaN dividends take the IEEE division instead (a branch that
-// continuous data never takes).  1 mul + 4 fma at full rate, instead of the v_div_scale /
-// quarter-rate v_rcp / v_div_fmas / v_div_fixup sequence and its hazard stalls.  Checked
-// against the IEEE quotient on 3.4e8 random dividends x 68 divisors (tools/div_rn_check.c).
-__device__ __forceinline__ double div_rn(double a, double b, double y) {
-  double q = a * y;
-  double e = __builtin_fma(-q, b, a);
-  q = __builtin_fma(e, y, q);
-  e = __builtin_fma(-q, b, a);
-  q = __builtin_fma(e, y, q);
-  const double m = __builtin_fabs(a);
-  if (!(m >= 0x1p-900 && m <= 0x1.fffffffffffffp+1023)) q = a / b;
-  return q;
-}
-
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

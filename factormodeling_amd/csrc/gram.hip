@@ -451,7 +451,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   constexpr int NEL = FP * SG_K;
   constexpr int EPT = (NEL + SG_NT - 1) / SG_NT;
   __shared__ double Zs[2][FP * SG_KP];
-  __shared__ double mu_s[2][FP], sd_s[2][FP], rs_s[2][FP];
+  __shared__ double mu_s[2][FP], sd_s[2][FP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t slice = blockIdx.x;
   const int64_t c0 = slice * total / nslice, c1 = (slice + 1) * total / nslice;
@@ -485,10 +485,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
     const int p = (int)(dr & 1);
     for (int r = tid; r < FP; r += SG_NT) {
       mu_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr)] : 0.0;
-      const double sd = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
-      sd_s[p][r] = sd;
-      const double rs = 1.0 / sd;                 // RN(1 / sd) for div_rn (0: IEEE divide)
-      rs_s[p][r] = (sd >= 0x1p-900 && rs >= 0x1p-900 && rs <= 0x1p+900) ? rs : 0.0;
+      sd_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
     }
   };
   // stage the chunk held in xr (global chunk index c, date dr) into buffer b
@@ -501,11 +498,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
       if (e >= NEL) continue;                     // wave-uniform (NEL is a multiple of 64)
       const double v = xr[u], sd = sd_s[p][r];
       const bool ok = (v == v) && (sd > 0.0);
-      // (v - mu) / sd bit-identically via the row's reciprocal (div_rn); sd is a normal
-      // positive number wherever ok (the row stats of a non-constant row)
-      const double rs = rs_s[p][r];
-      Zs[b][r * SG_KP + cl] =
-          ok ? ((opt & 1) && rs > 0.0 ? div_rn(v - mu_s[p][r], sd, rs) : (v - mu_s[p][r]) / sd) : 0.0;
+      Zs[b][r * SG_KP + cl] = ok ? (v - mu_s[p][r]) / sd : 0.0;
       const uint64_t bal = __ballot(ok);
       if ((lane & 31) == 0 && r < F) mbits[(uint32_t)c * (uint32_t)F + (uint32_t)r] = (uint32_t)(bal >> lane);
     }
@@ -692,7 +685,7 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   if (!mask_mfma && db) {
     const int64_t nch = ceil_div(A, (int64_t)SG_K);
     static const int exp = getenv("FMX_GRAM_EXP") ? atoi(getenv("FMX_GRAM_EXP")) : 0;   // timing only
-    // bit 0: z-score by div_rn with the row reciprocal, bit 1: MFMA / staging interleave
+    // bit 1: MFMA / staging interleave across each SIMD's waves (default; A/B switch)
     static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
     if (NB == 13 && exp == 1)
       k_gram_db<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);

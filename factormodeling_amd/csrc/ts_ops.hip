@@ -444,175 +444,6 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
   }
 }
 
-// k_ts_set with the VALU diet (same outputs bit for bit, ts_decay to BLAS-dot tolerance as
-// before).  The fused set is VALU-bound (~400 instructions per step with 7 IEEE divides),
-// so:
-//   * the six divides by small integers (Welford t / n on add and remove, the mean s / n,
-//     the variance ssq / (n - 1), the decay weight sum) use div_rn with reciprocals from
-//     an LDS table (rcp[n] = RN(1 / n)); only the z-score's divide by sigma stays IEEE;
-//   * ts_rank's value (less + (eq + 1) / 2) / WR depends only on k = 2 less + eq + 1, so it
-//     is read from an exact LDS table;
-//   * the decay dot runs on fma (numpy's BLAS ddot also fuses; parity is <= 1e-12 rel);
-//   * one workgroup row never straddles two factors (grid = (A / 256, F)), so each factor's
-//     six base pointers are wave-uniform (SGPRs) and one 32-bit byte offset per lane
-//     addresses all six streams (saddr + voffset forms; host requires D * ld * 8 < 2^32).
-template <int W, int WR>
-struct SetTab {
-  double rcp[W + 1];         // rcp[n] = RN(1 / n)
-  double rk[2 * WR + 2];     // rk[k] = (k / 2) / WR
-};
-
-template <int W, int WR>
-__device__ __forceinline__ void ts_set2_step(SetSt& c, double v, double* ring, int q, uint32_t ob,
-                                             const SetTab<W, WR>& tb, char* __restrict__ Ym, char* __restrict__ Ys,
-                                             char* __restrict__ Yz, char* __restrict__ Yr, char* __restrict__ Yd) {
-  if (c.first) { c.ms.init(v); c.vs.init(v); c.first = false; }
-  const bool full = c.i >= W;
-  const double old = full ? ring[q] : qnan();
-  const double oldr = (WR == W) ? old : ((c.i >= WR) ? ring[(q + W - WR) % W] : qnan());
-  ring[q] = v;
-  if (full) {
-    // MeanSt::remove then VarSt::remove with the reciprocal of the decremented count
-    c.ms.remove(old);
-    VarSt& s = c.vs;
-    if (old == old) {
-      s.n -= 1.0;
-      if (s.n != 0.0) {
-        const double pm = s.mean - s.cr;
-        const double y = old - s.cr;
-        const double t = y - s.mean;
-        s.cr = t + s.mean - y;
-        s.mean = s.mean - div_rn(t, s.n, tb.rcp[c.ms.n]);
-        s.ssq = s.ssq - (old - pm) * (old - s.mean);
-      } else {
-        s.mean = 0.0;
-        s.ssq = 0.0;
-      }
-    }
-  }
-  c.ms.add(v);
-  {
-    VarSt& s = c.vs;
-    if (v == v) {
-      s.n += 1.0;
-      if (v == s.prev) s.same += 1; else s.same = 1;
-      s.prev = v;
-      const double pm = s.mean - s.ca;
-      const double y = v - s.ca;
-      const double t = y - s.mean;
-      s.ca = t + s.mean - y;
-      s.mean = s.mean + div_rn(t, s.n, tb.rcp[c.ms.n]);
-      s.ssq = s.ssq + (v - pm) * (v - s.mean);
-    }
-  }
-  // MeanSt::result(W)
-  const int n = c.ms.n;
-  double m = qnan();
-  if (n >= W) {
-    m = div_rn(c.ms.s, (double)n, tb.rcp[n]);
-    if (c.ms.same >= n) m = c.ms.prev;
-    else if (c.ms.neg == 0 && m < 0) m = 0.0;
-    else if (c.ms.neg == n && m > 0) m = 0.0;
-  }
-  // VarSt::var(W, 1) -> zsqrt
-  double var = qnan();
-  if (c.vs.n >= (double)W && c.vs.n > 1.0) {
-    if (c.vs.n == 1.0 || (double)c.vs.same >= c.vs.n) var = 0.0;
-    else var = div_rn(c.vs.ssq, c.vs.n - 1.0, tb.rcp[n - 1]);
-  }
-  const double sd = zsqrt(var);
-  if (Ym) *reinterpret_cast<double*>(Ym + ob) = m;
-  if (Ys) *reinterpret_cast<double*>(Ys + ob) = sd;
-  if (Yz) *reinterpret_cast<double*>(Yz + ob) = (v - m) / (sd == 0.0 ? qnan() : sd);
-  if (full && old != old) c.nan_w -= 1;
-  if (c.i >= WR && oldr != oldr) c.nan_r -= 1;
-  if (v != v) { c.nan_w += 1; c.nan_r += 1; }
-  if (Yr) {
-    double o = qnan();
-    if (c.i + 1 >= WR && c.nan_r == 0) {
-      int k2 = 1;
-#pragma unroll
-      for (int k = 0; k < WR; ++k) {
-        const double w = ring[(q + W - k) % W];
-        k2 += (w < v) ? 2 : 0;
-        k2 += (w == v) ? 1 : 0;
-      }
-      o = tb.rk[k2];
-    }
-    *reinterpret_cast<double*>(Yr + ob) = o;
-  }
-  if (Yd) {
-    double o = qnan();
-    if (c.i + 1 >= W && c.nan_w == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);
-      constexpr double wsum = (double)W * (double)(W + 1) / 2.0;
-      constexpr double ywsum = 1.0 / wsum;
-      o = div_rn(acc, wsum, ywsum);
-    }
-    *reinterpret_cast<double*>(Yd + ob) = o;
-  }
-  c.i += 1;
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int W, int WR, int PF>
-__global__ void __launch_bounds__(256, TS_SET_WAVES)
-k_ts_set2(const double* __restrict__ X, double* __restrict__ Ym, double* __restrict__ Ys, double* __restrict__ Yz,
-          double* __restrict__ Yr, double* __restrict__ Yd, int64_t D, int64_t A, int64_t ld) {
-  static_assert(W % PF == 0 && WR >= 1 && WR <= W, "windows");
-  __shared__ SetTab<W, WR> tb;
-  const int tid = threadIdx.x;
-  if (tid <= W) tb.rcp[tid] = 1.0 / (double)(tid > 0 ? tid : 1);
-  if (tid < 2 * WR + 2) tb.rk[tid] = ((double)tid / 2.0) / (double)WR;
-  __syncthreads();
-  const int64_t a = (int64_t)blockIdx.x * 256 + tid;
-  if (a >= A) return;
-  const int64_t fo = (int64_t)blockIdx.y * D * ld * (int64_t)sizeof(double);   // uniform factor base
-  const char* xb = reinterpret_cast<const char*>(X) + fo;
-  char* ym = Ym ? reinterpret_cast<char*>(Ym) + fo : nullptr;
-  char* ys = Ys ? reinterpret_cast<char*>(Ys) + fo : nullptr;
-  char* yz = Yz ? reinterpret_cast<char*>(Yz) + fo : nullptr;
-  char* yr = Yr ? reinterpret_cast<char*>(Yr) + fo : nullptr;
-  char* yd = Yd ? reinterpret_cast<char*>(Yd) + fo : nullptr;
-  const uint32_t step = (uint32_t)(ld * (int64_t)sizeof(double));
-  uint32_t ob = (uint32_t)(a * (int64_t)sizeof(double));       // byte offset of the date being stored
-  SetSt c;
-  c.i = 0; c.nan_w = 0; c.nan_r = 0; c.first = true;
-  double ring[W];
-#pragma unroll
-  for (int q = 0; q < W; ++q) ring[q] = 0.0;
-  double pf[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q) pf[q] = q < D ? *reinterpret_cast<const double*>(xb + ob + q * step) : 0.0;
-  uint32_t obx = ob + PF * step;                                // byte offset of the next date to fetch
-  int64_t d0 = 0;
-  for (; d0 + W + PF <= D; d0 += W) {
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      const double v = pf[q % PF];
-      pf[q % PF] = *reinterpret_cast<const double*>(xb + obx);
-      obx += step;
-      ts_set2_step<W, WR>(c, v, ring, q, ob, tb, ym, ys, yz, yr, yd);
-      ob += step;
-    }
-  }
-  for (; d0 < D; d0 += W) {
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      const int64_t d = d0 + q;
-      if (d < D) {
-        const double v = pf[q % PF];
-        if (d + PF < D) pf[q % PF] = *reinterpret_cast<const double*>(xb + obx);
-        obx += step;
-        ts_set2_step<W, WR>(c, v, ring, q, ob, tb, ym, ys, yz, yr, yd);
-        ob += step;
-      }
-    }
-  }
-}
-
 // Dense panels, windows without a register ring (W not instantiated in k_ts_reg, e.g. the
 // C5 window of 60): the moment machines only need the value LEAVING the window, which on
 // a dense panel is x[d - W] -- re-read from memory instead of kept in a ring (a 60-deep
@@ -1055,16 +886,6 @@ extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, d
   for (int k = 0; k < 5; ++k) FMX_ARG(outs[k] != X, "outputs must not alias X");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   if (!present && window == 20 && rank_window == 10 && getenv("FMX_TS_SET_SPLIT") == nullptr) {
-    // k_ts_set2 (VALU diet) measured slower than k_ts_set at C2 (30.2 vs 28.6 ms,
-    // profiles/r02/kbench_w2_*.log): the set is bound by its 1-read / 5-write HBM stream,
-    // not by VALU.  Kept as an opt-in A/B variant.
-    static const bool v2 = getenv("FMX_TS_SET_V2") != nullptr;
-    if (v2 && (D + 40) * ld * (int64_t)sizeof(double) < ((int64_t)1 << 32) && F <= 65535) {
-      k_ts_set2<20, 10, 5><<<dim3((unsigned)ceil_div(A, 256), (unsigned)F), 256, 0, as_stream(stream)>>>(
-          X, Ymean, Ystd, Yzscore, Yrank, Ydecay, D, A, ld);
-      FMX_LAUNCH_CHECK("k_ts_set2");
-      return FMX_OK;
-    }
     void* args[] = {(void*)&X, (void*)&Ymean, (void*)&Ystd, (void*)&Yzscore, (void*)&Yrank, (void*)&Ydecay,
                     (void*)&F, (void*)&D, (void*)&A, (void*)&ld};
     FMX_HIP(hipLaunchKernel((const void*)k_ts_set<20, 10, 5>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args,

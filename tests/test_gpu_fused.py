@@ -242,9 +242,8 @@ def test_cs_rank2_matches_rank_winsor_ranks(dev, A):
 
 
 def test_ts_set_division_edge_values(dev):
-    """k_ts_set2 replaces the integer divides by reciprocal + fma corrections (div_rn) with
-    an IEEE fallback for zero / tiny / huge / non-finite dividends: bit-identical to the
-    single-op kernels (IEEE divides) on values that exercise every branch."""
+    """The fused rolling set is bit-identical to the single-op kernels on zero / signed-zero
+    / huge / subnormal-range / infinite values, exact ties and a large offset."""
     import torch
     import factormodeling_amd.engine as E
     rng = np.random.default_rng(17)
