@@ -439,7 +439,7 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
 // waves' MFMAs), issues the loads of chunk c+2, runs chunk c's MFMAs, then one barrier.
 // Slices are equal ranges of the flattened (date, 32-asset block) chunk sequence, one per
 // CU.  The row stats are double-buffered by date parity, loaded one date ahead.
-template <int NB, int EXP = 0>   // EXP: timing experiments (1 no LDS fragment reads, 2 no staging)
+template <int NB, bool ZIN>   // ZIN: X already holds the z-scores (cs_zscore output), stats unused
 __global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
           int64_t ld, int64_t d0, int64_t nch, int64_t total, int64_t nslice, double* __restrict__ part,
@@ -482,6 +482,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
     }
   };
   auto load_stats = [&](int64_t dr) {             // date d0 + dr into buffer dr & 1
+    if (ZIN) return;
     const int p = (int)(dr & 1);
     for (int r = tid; r < FP; r += SG_NT) {
       mu_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr)] : 0.0;
@@ -490,15 +491,21 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   };
   // stage the chunk held in xr (global chunk index c, date dr) into buffer b
   auto stage = [&](int64_t c, int64_t dr, int b) {
-    if (EXP & 2) return;
     const int p = (int)(dr & 1);
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
       const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
       if (e >= NEL) continue;                     // wave-uniform (NEL is a multiple of 64)
-      const double v = xr[u], sd = sd_s[p][r];
-      const bool ok = (v == v) && (sd > 0.0);
-      Zs[b][r * SG_KP + cl] = ok ? (v - mu_s[p][r]) / sd : 0.0;
+      const double v = xr[u];
+      bool ok;
+      if (ZIN) {                                  // finite z-score; NaN / +-inf (sigma 0) -> invalid
+        ok = (v - v) == 0.0;
+        Zs[b][r * SG_KP + cl] = ok ? v : 0.0;
+      } else {
+        const double sd = sd_s[p][r];
+        ok = (v == v) && (sd > 0.0);
+        Zs[b][r * SG_KP + cl] = ok ? (v - mu_s[p][r]) / sd : 0.0;
+      }
       const uint64_t bal = __ballot(ok);
       if ((lane & 31) == 0 && r < F) mbits[(uint32_t)c * (uint32_t)F + (uint32_t)r] = (uint32_t)(bal >> lane);
     }
@@ -534,13 +541,12 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
 #pragma unroll 1
     for (int ks = 0; ks < SG_K; ks += 4) {
       const int kk = ks + (lane >> 4);
-      const double a0 = (EXP & 1) ? Zs[b][(lane & 15) * SG_KP + kk] : 0.0;
 #pragma unroll
       for (int u = 0; u < BPW; ++u) {
         if (blk[u] < 0) continue;                 // wave-uniform
         const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
-        const double a = (EXP & 1) ? a0 : Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
-        const double bb = (EXP & 1) ? a0 : Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
+        const double a = Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
+        const double bb = Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
         gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
       }
     }
@@ -684,19 +690,17 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   static const bool db = getenv("FMX_GRAM_SINGLE_BUFFER") == nullptr;   // A/B switch
   if (!mask_mfma && db) {
     const int64_t nch = ceil_div(A, (int64_t)SG_K);
-    static const int exp = getenv("FMX_GRAM_EXP") ? atoi(getenv("FMX_GRAM_EXP")) : 0;   // timing only
     // bit 1: MFMA / staging interleave across each SIMD's waves (default; A/B switch)
     static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
-    if (NB == 13 && exp == 1)
-      k_gram_db<NB, 1><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
-    else if (NB == 13 && exp == 2)
-      k_gram_db<NB, 2><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
-    else if (NB == 13 && exp == 3)
-      k_gram_db<NB, 3><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
+    if (stats)
+      k_gram_db<NB, false><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
+                                                              mbits, gopt);
     else
-      k_gram_db<NB><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part, mbits, gopt);
+      k_gram_db<NB, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
+                                                             mbits, gopt);
     FMX_LAUNCH_CHECK("k_gram_db");
   } else {
+    if (!stats) { set_error("z-score input (stats == NULL) needs the default fused Gram path"); return FMX_ERR_UNSUPPORTED; }
     const int64_t dps2 = mask_mfma ? dps : ceil_div(d1 - d0, nslice);
     const int64_t ns2 = mask_mfma ? nslice : ceil_div(d1 - d0, dps2);
     k_gram_small<NB, 0><<<(unsigned)ns2, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, d1, dps2, part, mbits);
@@ -841,7 +845,7 @@ extern "C" int64_t fmx_gram_fused_work_bytes(int64_t F, int64_t D, int64_t A, in
 extern "C" fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F,
                                      int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate,
                                      void* work, int64_t work_bytes, void* stream) {
-  FMX_ARG(X && stats && G && N, "null pointer");
+  FMX_ARG(X && G && N, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
   if (F > 256) {
     set_error("fmx_gram_fused supports F <= 256; use fmx_zscore_exposures + fmx_gram");

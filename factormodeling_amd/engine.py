@@ -349,11 +349,12 @@ FUSED_GRAM_MAX_F = 256
 
 
 def gram_fused(X, stats, d0=0, d1=None):
-    """G, N straight from the raw panel with row stats (F <= 256): one pass over X."""
+    """G, N straight from the raw panel with row stats (F <= 256): one pass over X.
+    ``stats=None``: X already holds the z-scores (the cs_zscore output of the rows)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
-    if tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous():
+    if stats is not None and (tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous()):
         raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
     d1 = D if d1 is None else d1
     G = torch.empty((F, F), dtype=F64, device=X.device)

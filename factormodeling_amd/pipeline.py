@@ -108,17 +108,17 @@ def plan_ops(ops, be, fuse=True):
             wr = next(iter(WR)) if WR else w
             stages.append((f"ts_set:{w}:{wr}", ts))
             left = [o for o in left if o not in ts]
-    if fuse and hasattr(be, "cs_zscore_neutralize"):
-        pair = [("cs", "zscore", None), ("cs", "market_neutralize", None)]
-        if all(p in left for p in pair):
-            stages.append(("cs_zscore_neutralize", pair))
-            left = [o for o in left if o not in pair]
     if fuse and hasattr(be, "cs_rank_winsor"):
         pair = [("cs_rank", None, None), ("winsor", None, None)]
         if all(p in left for p in pair):
             stages.append(("cs_rank_winsor", pair))
             left = [o for o in left if o not in pair]
     stages += [(_op_key(*o), [o]) for o in left]
+    if fuse and hasattr(be, "cs_zscore_neutralize"):
+        # last: its cs_zscore output is still in its buffer when the Gram reads it
+        pair = [("cs", "zscore", None), ("cs", "market_neutralize", None)]
+        if all(p in left for p in pair):
+            stages = [st for st in stages if st[1][0] not in pair] + [("cs_zscore_neutralize", pair)]
     return stages
 
 
@@ -263,9 +263,12 @@ class EngineBackend:
         return E.cs_moment_stats("zscore", X, out=out)
 
     @staticmethod
-    def corr_gram(X, d0, d1, stats=None):
-        """G, N over dates [d0, d1): fused single pass for F <= 256, else Z/M + tiles."""
+    def corr_gram(X, d0, d1, stats=None, z=None):
+        """G, N over dates [d0, d1): fused single pass for F <= 256 (from ``z``, the
+        step's cs_zscore output, when given), else Z/M + tiles."""
         if X.shape[0] <= E.FUSED_GRAM_MAX_F:
+            if z is not None:
+                return E.gram_fused(z, None, d0, d1)
             if stats is None:
                 _, stats = E.cs_moment_stats("stats", X)
             return E.gram_fused(X, stats, d0, d1)
@@ -324,6 +327,8 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
         st = _stage_stream(name, streams)
         ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
         with ctx:
+            if side is not None and any(o is side.get("zscore") for o in outs):
+                side.pop("zscore")                   # about to be overwritten
             _run_stage(name, ops, outs, X, be, side, timers, collect, own)
     return bufs
 
@@ -337,6 +342,7 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
         st = be.cs_zscore_neutralize(X, outs)
         if side is not None:
             side["stats"] = st
+            side["zscore"] = outs[0]                # the Gram's z (valid until the buffer is reused)
     elif name == "cs_rank_winsor":
         if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
             # the ranks of X also feed the daily IC (no second ranking of the panel)
@@ -426,7 +432,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)
-            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
+            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
             _rec(timers, "gram", t0)
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
@@ -489,7 +495,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
             G.record_stream(torch.cuda.current_stream(G.device))
             N.record_stream(torch.cuda.current_stream(N.device))
         elif hasattr(be, "corr_gram"):
-            G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"))
+            G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
         else:
             Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
             G, N = be.gram(Z, M)

@@ -230,7 +230,9 @@ fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, in
 int64_t fmx_gram_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int32_t with_mask);
 /* Fused form for F <= 256: G and N straight from the raw panel X with the row stats of
  * fmx_cs_moment_stats (z = (x - mean) / sd where x is non-NaN and sd > 0, else 0; M the
- * same validity), one pass over X, both MFMA products in the same workgroup.  Returns
+ * same validity), one pass over X, both MFMA products in the same workgroup.  stats ==
+ * NULL: X already holds the z-scores (the fmx_cs_zscore output of the same rows: z is
+ * used where finite, else 0 / invalid -- the same Z and M).  Returns
  * FMX_ERR_UNSUPPORTED for F > 256 (use fmx_zscore_exposures + fmx_gram). */
 fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, double* N, int64_t F, int64_t D,
                           int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,

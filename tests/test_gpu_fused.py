@@ -107,7 +107,7 @@ def test_cs_fused_ragged(dev):
 def test_plan_ops_groups_the_c2_set():
     from factormodeling_amd import pipeline as PL
     stages = PL.plan_ops(PL.OPS, PL.ENGINE, True)
-    assert [s for s, _ in stages] == ["ts_set:20:10", "cs_zscore_neutralize", "cs_rank_winsor"]
+    assert [s for s, _ in stages] == ["ts_set:20:10", "cs_rank_winsor", "cs_zscore_neutralize"]
     assert sorted(o for _, ops in stages for o in ops) == sorted(PL.OPS)
     assert len(PL.plan_ops(PL.OPS, PL.ENGINE, False)) == len(PL.OPS)
 
@@ -285,3 +285,17 @@ def test_step_streams_match_sequential(dev):
         if hasattr(a[0][k], "cpu"):
             assert np.array_equal(a[0][k].cpu().numpy(), b[0][k].cpu().numpy(), equal_nan=True), k
     assert np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+@pytest.mark.parametrize("A", [700, 5000])
+def test_gram_from_zscore_equals_gram_from_stats(dev, A):
+    """The fused Gram from the cs_zscore output (the benchmarked step) equals the one that
+    z-scores the raw panel with the row stats: same Z, same validity, same sums."""
+    import factormodeling_amd.engine as E
+    import torch
+    X = torch.as_tensor(_cs_panel(A + 11, 5, 12, A), device=dev)
+    Yz, Yn, st = E.cs_zscore_neutralize(X, with_stats=True)
+    G1, N1 = E.gram_fused(X, st, 0, 12)
+    G2, N2 = E.gram_fused(Yz, None, 0, 12)
+    assert np.array_equal(N1.cpu().numpy(), N2.cpu().numpy())
+    assert np.array_equal(G1.cpu().numpy(), G2.cpu().numpy())
