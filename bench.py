@@ -50,14 +50,14 @@ def bytes_per_unit(stage, F, ranked=False):
         return 48.0
     if kind == "cs_zscore_neutralize":  # X once + two outputs
         return 24.0
-    if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u32)
-        return 28.0 if ranked else 24.0
-    if kind == "rank2":              # ranks-only pass: X once + the u32 doubled ranks
-        return 12.0
+    if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u16)
+        return 26.0 if ranked else 24.0
+    if kind == "rank2":              # ranks-only pass: X once + the u16 doubled ranks
+        return 10.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
         return 16.0
-    if kind == "ic_daily":              # X once (+ its u32 ranks when ranked) + two R rows
-        return (12.0 if ranked else 8.0) + 16.0 / F
+    if kind == "ic_daily":              # X once (+ its u16 ranks when ranked) + two R rows
+        return (10.0 if ranked else 8.0) + 16.0 / F
     return None
 
 

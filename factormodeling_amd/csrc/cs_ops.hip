@@ -796,7 +796,7 @@ extern "C" fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64
 
 extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D,
                                          int64_t A, int64_t ld, double qlo, double qhi, const uint8_t* present,
-                                         uint32_t* rank2, void* stream) {
+                                         fmx_rank2_t* rank2, void* stream) {
   FMX_ARG(X && Yrank && Ywinsor, "null panel");
   FMX_ARG(Yrank != X && Ywinsor != X && Yrank != Ywinsor, "outputs must be distinct from X and each other");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
@@ -810,7 +810,7 @@ extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double*
   return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
 }
 
-extern "C" fmx_status fmx_cs_rank2(const double* X, uint32_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
+extern "C" fmx_status fmx_cs_rank2(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
                                    void* stream) {
   FMX_ARG(X && rank2, "null panel");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");

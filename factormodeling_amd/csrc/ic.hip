@@ -323,7 +323,7 @@ extern "C" fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, 
 
 extern "C" int64_t fmx_ic_ranked_work_len(int64_t F, int64_t D) { return ic_ranked_work_len(F, D); }
 
-extern "C" fmx_status fmx_ic_daily_ranked(const double* X, const uint32_t* rank2, const double* R, int64_t F,
+extern "C" fmx_status fmx_ic_daily_ranked(const double* X, const fmx_rank2_t* rank2, const double* R, int64_t F,
                                           int64_t D, int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags,
                                           int32_t* work, int64_t work_len, double* out, void* stream) {
   FMX_ARG(X && rank2 && R && out && lags && work, "null pointer");

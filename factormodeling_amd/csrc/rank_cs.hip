@@ -26,7 +26,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   }
   double* Y2 = nullptr;
   double qlo = 0.0, qhi = 0.0;
-  uint32_t* RK = nullptr;
+  fmx_rank2_t* RK = nullptr;
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
@@ -40,7 +40,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
 // optionally the doubled ranks RK; returns FMX_ERR_UNSUPPORTED when the row does not fit
 // the fine kernel (caller splits).
 fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
-                             double qlo, double qhi, const uint8_t* present, uint32_t* RK, hipStream_t st) {
+                             double qlo, double qhi, const uint8_t* present, fmx_rank2_t* RK, hipStream_t st) {
   const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
@@ -58,7 +58,7 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
 
 // Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
 // raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
-fmx_status br_cs_rank2(const double* X, uint32_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
+fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
   const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);

@@ -45,13 +45,13 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 // statistic k (less <= k < less + equal) publishes its key -- no second pass over the row.
 //
 // RK (optional): 2 * average rank among the row's valid keys, i.e. 2*#less + #equal + 1
-// (0 for NaN / absent), as uint32 -- the daily IC of the same rows starts from it
+// (0 for NaN / absent), as uint16 (<= 2A) -- the daily IC of the same rows starts from it
 // (k_ic_wave) instead of ranking them again.
 template <int NT, int EMAX, bool PRES, bool WQ = false>
 __global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
-             uint32_t* __restrict__ RK) {
+             fmx_rank2_t* __restrict__ RK) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
@@ -118,7 +118,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (RK) {                                 // nv == 0 or a single-row date (rank 1)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) RK[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? 0u : 2u;
+        if (k < EMAX - 1 || last_in) RK[row * ld + t + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
     }
     if (WQ) {                                 // nv < 5: winsor is the identity
 #pragma unroll
@@ -212,7 +212,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     else r = (double)less + (double)(eq + 1) / 2.0;
     // write-once outputs: nontemporal stores
     if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den, y + t + k * NT);
-    if (RK) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1),
+    if (RK) __builtin_nontemporal_store((fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1)),
                                         RK + row * ld + t + k * NT);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
 #pragma unroll
@@ -730,7 +730,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
 // k_ic_daily_fr (same element order, same butterflies: the records are bit-identical).
 template <int NT, int EMAX>
 __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restrict__ X,
-                                              const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
+                                              const fmx_rank2_t* __restrict__ RK, const double* __restrict__ Rt,
                                               int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL,
                                               double* __restrict__ out) {
   constexpr int NW = NT / 64, ES = 64;
@@ -744,7 +744,7 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
   BR_PH_INIT;
   const int64_t s = row / F, f = row % F;
   const double* xf = X + (f * D + s) * ld;
-  const uint32_t* rkf = RK + (f * D + s) * ld;
+  const fmx_rank2_t* rkf = RK + (f * D + s) * ld;
   const int lagv[2] = {L0, L1};
   const double* rr[2];
   bool act[2];
@@ -934,7 +934,7 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
 // walks the list.
 template <int NT, int EMAX>
 __global__ void __launch_bounds__(NT, 4)
-k_ic_ranked_list(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt,
+k_ic_ranked_list(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, const double* __restrict__ Rt,
                  int64_t F, int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
                  const int32_t* __restrict__ list) {
   const int n = list[0];

@@ -97,7 +97,7 @@ constexpr int ICW_EC = 256;   // E entries per (wave, lag); more NaN returns: IC
 #define ICW_MINW 6
 #endif
 __global__ void __launch_bounds__(64 * ICW_WAVES, ICW_MINW)
-k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const double* __restrict__ Rt, int64_t F,
+k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, const double* __restrict__ Rt, int64_t F,
           int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
           const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
   // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64);
@@ -119,7 +119,7 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
   }
   if (!act[0] && !act[1]) return;
   const double* xf = X + (f * D + s) * ld;
-  const uint32_t* rkf = RK + (f * D + s) * ld;
+  const fmx_rank2_t* rkf = RK + (f * D + s) * ld;
   const int nb = (int)((2 * A) >> 6) + 1;     // doubled ranks are <= 2A
   const int nbp = (nb + 1) & ~1;
   uint32_t* T[2];
@@ -319,7 +319,7 @@ k_ic_wave(const double* __restrict__ X, const uint32_t* __restrict__ RK, const d
 // work: [D][ICW_PC] positions, [D] counts, [1 + F*D] overflow list.  A <= 16384.
 int64_t ic_ranked_work_len(int64_t F, int64_t D) { return D * (ICW_PC + 1) + 1 + F * D; }
 
-fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
+fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
                         int64_t ld, const int32_t* lags_host, int n_lags, double* out, int32_t* work, hipStream_t st) {
   const int nt = 1024;
   const void* kl = FMX_EMAX_TABLE(k_ic_ranked_list)(nt, br_emax(A, nt));

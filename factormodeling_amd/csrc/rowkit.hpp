@@ -324,13 +324,13 @@ constexpr int PW_LDS_MAX = 1024;
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
                       const uint8_t* present, hipStream_t st);
 fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
-                             double qlo, double qhi, const uint8_t* present, uint32_t* RK, hipStream_t st);
-fmx_status br_cs_rank2(const double* X, uint32_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st);
+                             double qlo, double qhi, const uint8_t* present, fmx_rank2_t* RK, hipStream_t st);
+fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st);
 fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                           double qlo, double qhi, const uint8_t* present, hipStream_t st);
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                        const int32_t* lags_host, int n_lags, double* out, hipStream_t st);
-fmx_status br_ic_ranked(const double* X, const uint32_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
+fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
                         int64_t ld, const int32_t* lags_host, int n_lags, double* out, int32_t* work, hipStream_t st);
 int64_t ic_ranked_work_len(int64_t F, int64_t D);
 

@@ -149,6 +149,7 @@ def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=Fal
 
 
 RANKED_IC_MAX_A = 16384
+RANK2_DTYPE = torch.int16   # fmx_rank2_t: doubled ranks <= 2A as uint16 bit patterns
 BITONIC_RANK_MAX_A = 8192   # fmx_cs_rank's LDS bitonic path (methods first / dense)
 _WORK = {}
 
@@ -173,7 +174,7 @@ def _workspace_bytes(device, nbytes):
 
 def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, present=None, rank2=None):
     """cs_rank(average) and cs_winsor(qlo, qhi) in one pass (fmx_cs_rank_winsor).
-    ``rank2`` (uint32 tensor shaped like X): also the doubled ranks that
+    ``rank2`` (int16 tensor shaped like X, bit pattern uint16): also the doubled ranks that
     ``ic_daily(..., rank2=)`` starts from."""
     X = as3(X)
     _check_panel(X)
@@ -181,8 +182,8 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
     _check_present(present, D, A)
     Yr, Yw = _out(X, out_rank), _out(X, out_winsor)
     if rank2 is not None:
-        if rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
-            raise _lib.FmxError("rank2 must be a contiguous int32 (bit pattern uint32) [F][D][A] tensor")
+        if rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+            raise _lib.FmxError("rank2 must be a contiguous int16 (bit pattern uint16) [F][D][A] tensor")
     call("fmx_cs_rank_winsor", ptr(X), ptr(Yr), ptr(Yw), F, D, A, A, float(qlo), float(qhi), ptr(present),
          ptr(rank2), stream_ptr())
     return Yr, Yw
@@ -195,9 +196,9 @@ def cs_rank2(X, rank2=None):
     _check_panel(X)
     F, D, A = X.shape
     if rank2 is None:
-        rank2 = torch.empty((F, D, A), dtype=torch.int32, device=X.device)
-    elif rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
-        raise _lib.FmxError("rank2 must be a contiguous int32 [F][D][A] tensor")
+        rank2 = torch.empty((F, D, A), dtype=RANK2_DTYPE, device=X.device)
+    elif rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+        raise _lib.FmxError("rank2 must be a contiguous int16 [F][D][A] tensor")
     call("fmx_cs_rank2", ptr(X), ptr(rank2), F, D, A, A, stream_ptr())
     return rank2
 
@@ -290,8 +291,8 @@ def ic_daily(X, R, lags=(1,), rank2=None):
     lag_h = (ctypes.c_int32 * len(lags))(*[int(v) for v in lags])
     out = torch.empty((len(lags), 4, F, D), dtype=F64, device=X.device)
     if rank2 is not None:
-        if rank2.dtype != torch.int32 or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
-            raise _lib.FmxError("rank2 must be a contiguous int32 [F][D][A] tensor")
+        if rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+            raise _lib.FmxError("rank2 must be a contiguous int16 [F][D][A] tensor")
         n = int(_lib.load().fmx_ic_ranked_work_len(F, D))
         work = _workspace(X.device, n)
         call("fmx_ic_daily_ranked", ptr(X), ptr(rank2), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p),

@@ -348,7 +348,7 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
             # the ranks of X also feed the daily IC (no second ranking of the panel)
             rk = side.get("rank2_buf")
             if rk is None or tuple(rk.shape) != tuple(X.shape):
-                rk = torch.empty(X.shape, dtype=torch.int32, device=X.device)
+                rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=X.device)
             side["rank2"] = rk
             be.cs_rank_winsor(X, outs, rank2=rk)
         else:
@@ -442,7 +442,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         t0 = _ev(timers)
         rk = getattr(sp, "rank2", None)
         if rk is None:
-            rk = torch.empty(sp.X.shape, dtype=torch.int32, device=sp.X.device)
+            rk = torch.empty(sp.X.shape, dtype=E.RANK2_DTYPE, device=sp.X.device)
         be.cs_rank2(sp.X, rk)
         side["rank2"] = rk
         _rec(timers, "rank2", t0)

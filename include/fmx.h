@@ -31,6 +31,10 @@
 
 #include <stdint.h>
 
+/* Doubled average rank of a cell among its row's non-NaN cells (2*#less + #equal + 1; 0
+ * for NaN): <= 2A <= 32768 for the A <= 16384 rows the ranked kernels take, so 16 bits. */
+typedef uint16_t fmx_rank2_t;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -146,11 +150,11 @@ fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t
 /* cs_rank(method='average') and cs_winsor(limits=(qlo, qhi)) of the same rows in ONE pass
  * (operations.py:54-68): the winsor quantiles' order statistics are read off the rank
  * histogram.  Outputs bit-identical to fmx_cs_rank / fmx_cs_winsor; distinct from X.
- * rank2 (optional, device uint32 [F][D][ld], needs present == NULL and A <= 16384): the
+ * rank2 (optional, device fmx_rank2_t [F][D][ld], needs present == NULL and A <= 16384): the
  * doubled average rank of every non-NaN cell (2*#less + #equal + 1; 0 for NaN), the input
  * of fmx_ic_daily_ranked. */
 fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
-                              int64_t ld, double qlo, double qhi, const uint8_t* present, uint32_t* rank2,
+                              int64_t ld, double qlo, double qhi, const uint8_t* present, fmx_rank2_t* rank2,
                               void* stream);
 /* cs_rank(method='first' | 'dense') for any row length (A <= 65535): rows sorted in HBM
  * (rocPRIM segmented radix sort of (value key, asset) pairs, stable), then one workgroup
@@ -159,10 +163,10 @@ fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, i
 fmx_status fmx_cs_rank_sorted(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
                               const uint8_t* present, void* work, int64_t work_bytes, void* stream);
 int64_t fmx_cs_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
-/* Only the doubled average ranks of fmx_cs_rank_winsor (rank2 [F][D][ld] uint32, A <=
+/* Only the doubled average ranks of fmx_cs_rank_winsor (rank2 [F][D][ld] fmx_rank2_t, A <=
  * 16384): the rank pass of a daily IC over raw factors (fmx_ic_daily_ranked) when no
  * operator output of the same rows is wanted (factor_selector.py:36-48's rankdata). */
-fmx_status fmx_cs_rank2(const double* X, uint32_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
+fmx_status fmx_cs_rank2(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
                         void* stream);
 /* cs_winsor (operations.py:64-68); qlo/qhi are the fractions numpy sees
  * (pandas passes q*100 and numpy divides by 100). */
@@ -199,7 +203,7 @@ fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, 
  * agree with fmx_ic_daily to ~1e-15 relative, pair counts exactly).  work: device int32
  * scratch of fmx_ic_ranked_work_len(F, D) elements.  A <= 16384. */
 int64_t fmx_ic_ranked_work_len(int64_t F, int64_t D);
-fmx_status fmx_ic_daily_ranked(const double* X, const uint32_t* rank2, const double* R, int64_t F, int64_t D,
+fmx_status fmx_ic_daily_ranked(const double* X, const fmx_rank2_t* rank2, const double* R, int64_t F, int64_t D,
                                int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags, int32_t* work,
                                int64_t work_len, double* out, void* stream);
 /* Window summaries of one lag's daily stats [4][F][D] over J date windows [d0, d1).

@@ -140,7 +140,7 @@ def test_ic_ranked_matches_standalone_ic(dev, A, r_nan, lags):
     F, D = (3, 9) if A <= 5000 else (2, 8)
     X, R = _ic_case(A + len(lags), F, D, A, r_nan)
     Xt, Rt = torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev)
-    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
     E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
     got = E.ic_daily(Xt, Rt, lags, rank2=rk).cpu().numpy()
     ref = E.ic_daily(Xt, Rt, lags).cpu().numpy()
@@ -157,9 +157,9 @@ def test_rank2_is_doubled_average_rank(dev):
     X[1, 2] = np.nan
     X[1, 3, 1:] = np.nan                       # single valid value
     Xt = torch.as_tensor(X, device=dev)
-    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
     E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
-    got = rk.cpu().numpy()
+    got = rk.cpu().numpy().view(np.uint16)
     for f in range(2):
         for d in range(6):
             x = X[f, d]
@@ -176,7 +176,7 @@ def test_rank2_rejects_presence_mask(dev):
     from factormodeling_amd._lib import FmxError
     X = torch.zeros((1, 3, 10), dtype=torch.float64, device=dev)
     pres = torch.ones((3, 10), dtype=torch.uint8, device=dev)
-    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
     with pytest.raises(FmxError):
         E.cs_rank_winsor(X, 0.01, 0.99, present=pres, rank2=rk)
 
@@ -215,7 +215,7 @@ def test_ic_ranked_long_rows_vs_oracle(dev):
     Xt, Rt = torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev)
     with pytest.raises(FmxError):
         E.ic_daily(Xt, Rt, (1,))
-    rk = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
     E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
     got = E.ic_daily(Xt, Rt, (1, 2), rank2=rk).cpu().numpy()
     for m, L in enumerate((1, 2)):
@@ -235,7 +235,7 @@ def test_cs_rank2_matches_rank_winsor_ranks(dev, A):
     X[1, 2] = np.nan                           # empty row
     X[1, 3, 1:] = np.nan                       # single valid value
     Xt = torch.as_tensor(X, device=dev)
-    ref = torch.empty(X.shape, dtype=torch.int32, device=dev)
+    ref = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
     E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=ref)
     got = E.cs_rank2(Xt)
     assert np.array_equal(got.cpu().numpy(), ref.cpu().numpy())

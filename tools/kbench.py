@@ -68,7 +68,7 @@ _RK = {}
 def _rank2(X):
     """doubled ranks of X (made once, by the fused rank pass)."""
     if "rk" not in _RK:
-        _RK["rk"] = torch.empty(X.shape, dtype=torch.int32, device=X.device)
+        _RK["rk"] = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=X.device)
         E.cs_rank_winsor(X, 0.01, 0.99, rank2=_RK["rk"])
     return _RK["rk"]
 
@@ -87,8 +87,8 @@ OPS = {
     "ts_set": (lambda X, R, Y: E.ts_set(X, _set_outs(X), 20, 10), 48),
     "cs_zn": (lambda X, R, Y: E.cs_zscore_neutralize(X, Y, _set_outs(X)["mean"]), 24),
     "cs_rw": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"]), 24),
-    "cs_rw_rk": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"], rank2=_rank2(X)), 28),
-    "ic_ranked": (lambda X, R, Y: E.ic_daily(X, R, (1, 2), rank2=_rank2(X)), 12),
+    "cs_rw_rk": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"], rank2=_rank2(X)), 26),
+    "ic_ranked": (lambda X, R, Y: E.ic_daily(X, R, (1, 2), rank2=_rank2(X)), 10),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
     "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
     "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
