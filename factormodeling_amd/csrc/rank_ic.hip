@@ -88,8 +88,8 @@ k_nan_positions(const double* __restrict__ Rt, int64_t D, int64_t A, int64_t ld,
 // Moments are single-pass about the first pair (rank moments from exact integer sums), so
 // records agree with the two-pass kernels to ~1e-15 relative, not bitwise.
 constexpr int ICW_WAVES = 4;
-#ifndef ICW_UNROLL
-#define ICW_UNROLL 1
+#ifndef ICW_PF
+#define ICW_PF 1
 #endif
 constexpr int ICW_EC = 256;   // E entries per (wave, lag); more NaN returns: ICW_PC overflow
 
@@ -217,15 +217,33 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
 #pragma unroll
     for (int q = 0; q < 6; ++q) sm[m][q] = 0.0;
   const int An = (int)A;
-#pragma unroll ICW_UNROLL
-  for (int i0 = 0; i0 < An; i0 += 64) {
+  // software pipeline, ICW_PF chunks deep: the loads of chunks i+1..i+ICW_PF are in flight
+  // while chunk i is reduced (one wave per row: without it every chunk waits a full HBM
+  // latency and only other waves hide it)
+  double xq[ICW_PF], rq[ICW_PF][2];
+  uint32_t kq[ICW_PF];
+  auto load = [&](int i0, int s) {
     const int i = i0 + lane;
     const bool in = i < An;
-    const double x = in ? xf[i] : qnan();
-    const uint32_t rk = in ? rkf[i] : 0u;
-    double r[2];
+    xq[s] = in ? xf[i] : qnan();
+    kq[s] = in ? (uint32_t)rkf[i] : 0u;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) r[m] = (in && act[m]) ? rr[m][i] : qnan();
+    for (int m = 0; m < 2; ++m) rq[s][m] = (in && act[m]) ? rr[m][i] : qnan();
+  };
+#pragma unroll
+  for (int s = 0; s < ICW_PF; ++s) load(64 * s, s);
+  for (int i0 = 0; i0 < An; i0 += 64) {
+    const double x = xq[0];
+    const uint32_t rk = kq[0];
+    double r[2] = {rq[0][0], rq[0][1]};
+#pragma unroll
+    for (int s = 0; s + 1 < ICW_PF; ++s) {   // rotate (register renames)
+      xq[s] = xq[s + 1];
+      kq[s] = kq[s + 1];
+      rq[s][0] = rq[s + 1][0];
+      rq[s][1] = rq[s + 1][1];
+    }
+    if (i0 + 64 * ICW_PF < An) load(i0 + 64 * ICW_PF, ICW_PF - 1);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const bool p = x == x && r[m] == r[m];
