@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-2 profile set: kernel stats of the default bench (C2) and the C4 bench, FETCH /
+# Profile set: kernel stats of the default bench (C2) and the C4 bench, FETCH /
 # WRITE passes over the C2 kernels (kbench; ts_mean calibrates FETCH_SIZE), and an MFMA
 # pass over the wide Gram (kbench, C4 factors/assets on 252 dates).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-T=${1:-r2}
+T=${1:-prof}
 KOPS="ts_mean,ts_set,cs_zn,cs_rw_rk,ic_ranked,gram"
 trap 'find gpurun_out -name "*kernel_trace.csv" -size +2M -delete; find gpurun_out -name "*agent_info.csv" -delete' EXIT
 tools/gpu_run.sh \
