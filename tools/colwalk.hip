@@ -94,6 +94,35 @@ __global__ void __launch_bounds__(256) walk1nt(const double* __restrict__ X, dou
   }
 }
 
+// walk2 with nontemporal loads / stores
+template <int NOUT, int PF>
+__global__ void __launch_bounds__(256) walk2nt(const double* __restrict__ X, double* __restrict__ Y, long F, long D,
+                                               long A, long ld, long ostride) {
+  const long A2 = A / 2;
+  const long col = (long)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A2) return;
+  const long f = col / A2, a = (col - f * A2) * 2;
+  const dbl2* x = reinterpret_cast<const dbl2*>(X + f * D * ld + a);
+  dbl2* y = reinterpret_cast<dbl2*>(Y + f * D * ld + a);
+  const long l2 = ld / 2, o2 = ostride / 2;
+  dbl2 pf[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) pf[q] = __builtin_nontemporal_load(x + q * l2);
+  dbl2 acc = {0.0, 0.0};
+  for (long d = 0; d < D; d += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const dbl2 v = pf[q];
+      if (d + q + PF < D) pf[q] = __builtin_nontemporal_load(x + (d + q + PF) * l2);
+      acc += v;
+      if (d + q < D) {
+#pragma unroll
+        for (int o = 0; o < NOUT; ++o) __builtin_nontemporal_store(acc * (double)(o + 1), y + o * o2 + (d + q) * l2);
+      }
+    }
+  }
+}
+
 // walk2 with NT-thread blocks kept in lockstep (a barrier every PF dates), so that each
 // date step of a block reads / writes NT * 16 contiguous bytes at about the same time
 template <int NOUT, int PF, int NT>
@@ -170,6 +199,8 @@ int main() {
   rep("walk2 out5 pf5", 5, timeit([&] { walk2<5, 5><<<g2, 256>>>(X, Y, F, D, A, ld, n); }, 3));
   rep("walk2 out2 pf5", 2, timeit([&] { walk2<2, 5><<<g2, 256>>>(X, Y, F, D, A, ld, n); }, 3));
   rep("walk1 out2 pf5", 2, timeit([&] { walk1<2, 5><<<g1, 256>>>(X, Y, F, D, A, ld, n); }, 3));
+  rep("walk2nt out5 pf5", 5, timeit([&] { walk2nt<5, 5><<<g2, 256>>>(X, Y, F, D, A, ld, n); }, 3));
+  rep("walk2nt out5 pf2", 5, timeit([&] { walk2nt<5, 2><<<g2, 256>>>(X, Y, F, D, A, ld, n); }, 3));
   rep("walk1nt out5 pf5", 5, timeit([&] { walk1nt<5, 5><<<g1, 256>>>(X, Y, F, D, A, ld, n); }, 3));
   rep("walk1nt out1 pf5", 1, timeit([&] { walk1nt<1, 5><<<g1, 256>>>(X, Y, F, D, A, ld, n); }, 3));
   auto g2s = [&](int nt) { return (unsigned)((F * A / 2 + nt - 1) / nt); };
