@@ -187,28 +187,41 @@ class ShardedPanel:
             self.X, self.R = Xo, Ro
         self.own = self.d_hi - self.d_lo
 
-    def exchange_halo(self):
-        """Send my last ``halo`` owned dates to rank+1, receive rank-1's into my halo
-        (RCCL point-to-point over xGMI; gloo on CPU)."""
+    def exchange_halo_start(self):
+        """Post the halo exchange: send my last ``halo`` owned dates to rank+1, receive
+        rank-1's (RCCL point-to-point over xGMI; gloo on CPU).  Asynchronous: work that
+        needs no halo row runs while the transfer is in flight; exchange_halo_finish()
+        waits and writes the received rows into the halo."""
         if self.world == 1:
-            return
+            return None
         H = self.halo_len
-        reqs = []
+        reqs, bufs = [], []
         if self.rank + 1 < self.world:
             send_x = self.X[:, -H:].contiguous()
             send_r = self.R[-H:].contiguous()
+            bufs += [send_x, send_r]
             reqs.append(dist.isend(send_x, self.rank + 1))
             reqs.append(dist.isend(send_r, self.rank + 1))
+        recv = None
         if self.rank > 0:
-            recv_x = torch.empty((self.F, self.halo, self.A), dtype=self.X.dtype, device=self.X.device)
-            recv_r = torch.empty((self.halo, self.A), dtype=self.R.dtype, device=self.R.device)
-            reqs.append(dist.irecv(recv_x, self.rank - 1))
-            reqs.append(dist.irecv(recv_r, self.rank - 1))
+            recv = (torch.empty((self.F, self.halo, self.A), dtype=self.X.dtype, device=self.X.device),
+                    torch.empty((self.halo, self.A), dtype=self.R.dtype, device=self.R.device))
+            reqs.append(dist.irecv(recv[0], self.rank - 1))
+            reqs.append(dist.irecv(recv[1], self.rank - 1))
+        return reqs, recv, bufs
+
+    def exchange_halo_finish(self, handle):
+        if handle is None:
+            return
+        reqs, recv, _ = handle
         for r in reqs:
             r.wait()
-        if self.rank > 0:
-            self.X[:, :self.halo] = recv_x
-            self.R[:self.halo] = recv_r
+        if recv is not None:
+            self.X[:, :self.halo] = recv[0]
+            self.R[:self.halo] = recv[1]
+
+    def exchange_halo(self):
+        self.exchange_halo_finish(self.exchange_halo_start())
 
 
 class EngineBackend:
@@ -305,7 +318,7 @@ def _stage_stream(name, streams):
 
 
 def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None,
-            streams=None):
+            streams=None, only=None):
     """Operator set over the local panel (halo rows included as warm-up), as planned by
     ``plan_ops``; every operator writes its own output buffer (``bufs``: a list of tensors
     shaped like X, reused across steps).  Sequentially, stages share the buffers (as many
@@ -313,7 +326,7 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     stage gets its own.  ``collect`` (a dict) receives a copy of every operator's
     owned-date output (tests only); ``side`` (a dict) receives by-products later stages
     reuse (cs_zscore's row stats; "rank2", the doubled ranks of X, written into
-    side["rank2_buf"] when it fits)."""
+    side["rank2_buf"] when it fits).  ``only``: run just the stages it accepts (by name)."""
     stages = plan_ops(cfg.ops, be, cfg.fuse)
     offs, need = [], 0
     for _, ops in stages:
@@ -323,6 +336,8 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     while len(bufs) < need:
         bufs.append(torch.empty_like(X))
     for (name, ops), off in zip(stages, offs):
+        if only is not None and not only(name):
+            continue
         outs = bufs[off:off + len(ops)]
         st = _stage_stream(name, streams)
         ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
@@ -411,11 +426,28 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     """One pass of the hot path.  Returns (selected weights [J][F] (every rank holds the
     full result; None without selection), kept factor list (None without the Gram)).
     ``collect`` (tests) receives intermediate results."""
-    t0 = _ev(timers)
-    sp.exchange_halo()
-    _rec(timers, "halo", t0)
     side = {"rank2_buf": getattr(sp, "rank2", None)}   # filled as "rank2" when this step ranks X
     streams = None
+    early = not cfg.streams
+    t0 = _ev(timers)
+    halo = sp.exchange_halo_start()
+    _rec(timers, "halo", t0)
+    GN = None
+    if early:
+        # while the halo is in flight: the stages whose owned-date results read no halo
+        # row -- cs_zscore + market_neutralize (per-date rows) and the Gram over the owned
+        # dates (from that z-score).  They also process the halo rows, whose outputs are
+        # not owned (stale until the exchange lands: the same data every step).
+        if cfg.ops:
+            sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                              own=slice(sp.halo, None), side=side, only=lambda n: n == "cs_zscore_neutralize")
+        if cfg.gram and hasattr(be, "corr_gram"):
+            t0 = _ev(timers)
+            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
+            _rec(timers, "gram", t0)
+    t0 = _ev(timers)
+    sp.exchange_halo_finish(halo)
+    _rec(timers, "halo_wait", t0)
     if cfg.streams and cfg.ops and hasattr(be, "ts_set") and sp.X.is_cuda:
         # fork: the rolling set and the cs_zscore -> Gram chain on side streams, the rank
         # pass -> IC -> selection chain on the current one; joined before the Gram sum
@@ -427,8 +459,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
             st.wait_stream(main)
     if cfg.ops:
         sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                          own=slice(sp.halo, None), side=side, streams=streams)
-    GN = None
+                          own=slice(sp.halo, None), side=side, streams=streams,
+                          only=(lambda n: n != "cs_zscore_neutralize") if early else None)
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)

@@ -29,7 +29,8 @@ def _run(rank, world, port, q, skip_halo=False):
         be = OracleBackend()
         sp = PL.ShardedPanel(D, A, F, rank, world, torch.device("cpu"), seed=3)
         if skip_halo:
-            sp.exchange_halo = lambda: None          # negative control
+            sp.exchange_halo_start = lambda: None    # negative control: no exchange
+            sp.exchange_halo_finish = lambda h: None
         col = {}
         w, kept = PL.run_step(sp, cfg, be=be, collect=col)
         ops = {k: v.numpy() for k, v in col.items() if ":" in k}
