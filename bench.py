@@ -63,7 +63,7 @@ def bytes_per_unit(stage, F, ranked=False):
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
-                "ts_set": ("fmx::k_ts_set2<", "fmx::k_ts_set<"), "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
+                "ts_set": "fmx::k_ts_set<", "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",
