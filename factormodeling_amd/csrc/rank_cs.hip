@@ -15,7 +15,7 @@ template <int NT, int E> constexpr auto kcrw_pres = k_cs_rank_fa<NT, E, true, tr
 fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int method,
                       const uint8_t* present, hipStream_t st) {
   const int nt = br_nt(1024);
-  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const void* kfr = present ? FMX_EMAX_TABLE(kcr_pres)(nt_fa, br_emax(A, nt_fa))
                             : FMX_EMAX_TABLE(kcr_dense)(nt_fa, br_emax(A, nt_fa));
@@ -41,7 +41,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
 // the fine kernel (caller splits).
 fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F, int64_t D, int64_t A, int64_t ld,
                              double qlo, double qhi, const uint8_t* present, fmx_rank2_t* RK, hipStream_t st) {
-  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
   const void* k = present ? FMX_EMAX_TABLE(kcrw_pres)(nt_fa, E) : FMX_EMAX_TABLE(kcrw_dense)(nt_fa, E);
@@ -59,7 +59,7 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
 // Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
 // raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
 fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
-  const int nt_fa = fa_nt() == 1024 ? 1024 : 512;
+  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense)(nt_fa, E);

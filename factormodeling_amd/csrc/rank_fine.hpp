@@ -18,6 +18,17 @@ namespace fmx {
 #ifndef FR_FA_WAVES
 #define FR_FA_WAVES(NT) ((NT) == 1024 ? 8 : ((NT) == 640 ? 8 : 6))
 #endif
+// ... but no more than the LDS lets in: a row stages up to EMAX*NT 8-byte keys (at least
+// the 32 KB counter array), so long rows (EMAX*NT > 6144) hold one or two rows per CU
+// (two up to ~15/16 of EMAX*NT: C5's 10,000 assets in <1024,10>).  Asking for more waves
+// than can be resident only caps the VGPRs and spills the key registers
+// (k_cs_rank_fa<512,20>: 340 B/lane of scratch at a fixed 6-wave bound).
+constexpr int fr_fa_min_waves(int nt, int emax) {
+  const int dyn = emax * nt * 8 > 32768 ? emax * nt * 8 : 32768;
+  const int rows = (160 * 1024) / (dyn / 16 * 15 + 2048);
+  const int w = rows * nt / 256;
+  return w < 1 ? 1 : (w > FR_FA_WAVES(nt) ? FR_FA_WAVES(nt) : w);
+}
 // Scheduling fence between unrolled per-element steps: bounds how many elements' live
 // ranges overlap (register pressure at 8 waves/SIMD) -- other waves hide the latency.
 #ifndef FR_NO_SCHED_FENCE
@@ -48,7 +59,7 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 // (0 for NaN / absent), as uint16 (<= 2A) -- the daily IC of the same rows starts from it
 // (k_ic_wave) instead of ranking them again.
 template <int NT, int EMAX, bool PRES, bool WQ = false>
-__global__ void __launch_bounds__(NT, FR_FA_WAVES(NT))
+__global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
              fmx_rank2_t* __restrict__ RK) {

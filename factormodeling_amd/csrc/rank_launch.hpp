@@ -103,14 +103,17 @@ static inline fmx_status launch_persistent(const void* k, int nt, int64_t nrows,
     default: return (const void*)nullptr;                                    \
   }
 
-// Workgroup size of the aliased-LDS cs_rank kernel (FMX_FA_NT=512|640|1024).
-static inline int fa_nt() {
+// Workgroup size of the aliased-LDS cs_rank kernel for rows of A assets: 512 up to 8192
+// assets, 1024 beyond (a row's keys fill half the CU's LDS there, so 16 waves per row
+// instead of 8 -- C5's 10,000-asset rank pass: 287 -> 142 ms, profiles/r02/c5_h6.log).
+// FMX_FA_NT=512|640|1024 forces one size.
+static inline int fa_nt(int64_t A) {
   static int v = [] {
     const char* e = getenv("FMX_FA_NT");
     const int x = e ? atoi(e) : 0;
-    return (x == 512 || x == 640 || x == 1024) ? x : 512;
+    return (x == 512 || x == 640 || x == 1024) ? x : 0;
   }();
-  return v;
+  return v ? v : (A > 8192 ? 1024 : 512);
 }
 
 #define FMX_EMAX_TABLE3(KT)                                                  \

@@ -20,6 +20,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 import contextlib
+import os
 
 import numpy as np
 import torch
@@ -249,10 +250,10 @@ class EngineBackend:
 
     ranked_ic_max_a = E.RANKED_IC_MAX_A
 
-    # the ranks-only pass stages a row's keys in LDS (8 B per asset): past ~6k assets a CU
-    # holds one row, and rank pass + wave IC (C5, 10,000 assets: 420 + 76 ms) loses to the
-    # standalone IC kernel (227 ms), profiles/r02/c5_h1.log
-    rank_pass_max_a = 6144
+    # ranks-only pass + wave IC vs the standalone IC kernel at C5's 10,000 assets:
+    # 142 + 43 ms vs 226 ms (profiles/r02/c5_h6.log; was 420 + 76 ms before the rank
+    # kernel's LDS-aware launch bounds and 1024-thread rows, c5_h1.log)
+    rank_pass_max_a = int(os.environ.get("FMX_RANK_PASS_MAX_A", "16384"))
 
     @staticmethod
     def cs_rank2(X, rank2):
