@@ -913,8 +913,10 @@ extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* O
   if (!present && getenv("FMX_TS_LDS") == nullptr) {   // dense: leaving values re-read
     void* rargs[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
                      (void*)&y_fstride, (void*)&W};
-    FMX_HIP(hipLaunchKernel((const void*)k_ts_corr_rl<4>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0,
-                            as_stream(stream)));
+    // two dates of the four streams in flight: 116 VGPRs, 4 waves/SIMD (four dates: 154
+    // VGPRs, 3 waves, 160 vs 156 ms at C5; eight: 180 ms; forcing 4-5 waves spills)
+    const void* kc = (const void*)k_ts_corr_rl<2>;
+    FMX_HIP(hipLaunchKernel(kc, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, as_stream(stream)));
     return FMX_OK;
   }
   dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
