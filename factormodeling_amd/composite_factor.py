@@ -60,43 +60,57 @@ def weighted_plan(pdate, W, names):
     W = np.asarray(W, dtype=np.float64)
     J, F = W.shape
     suffix = np.array([engine.suffix_code(n) for n in names], dtype=np.int32)
-    pref = [n.split("_", 1)[0] for n in names]
+    _, pid = np.unique(np.array([n.split("_", 1)[0] for n in names], dtype=object).astype(str),
+                       return_inverse=True)
+    P = int(pid.max()) + 1 if F else 1
     sel = W > 0
     KMAX = int(max(1, sel.sum(axis=1).max() if J else 1))
+    sel &= (np.asarray(pdate) >= 0)[:, None]
     col = np.zeros((J, KMAX), np.int32)
     suf = np.zeros((J, KMAX), np.int32)
     grp = np.full((J, KMAX), -1, np.int32)
     gwa = np.zeros((J, KMAX), np.float64)
-    ncol = np.zeros(J, np.int32)
-    ngrp = np.zeros(J, np.int32)
-    pd_out = np.full(J, -1, np.int32)
-    soff = [0]
-    scol = []
-    for j in range(J):
-        cs = np.flatnonzero(sel[j]) if pdate[j] >= 0 else np.zeros(0, np.int64)
-        if cs.size:
-            gid, members, gs = {}, [], []
-            for c in cs:
-                g = gid.setdefault(pref[c], len(gid))
-                if g == len(members):
-                    members.append([])
-                members[g].append(c)
-                gs.append(g)
-            gsum = [W[j, m].sum() for m in members]   # pandas Series.sum = numpy sum (:281)
-            tot = sum(gsum)                           # Python sum (:282)
-            gw = [x / tot for x in gsum] if tot > 0 else [1 / len(gsum)] * len(gsum)
-            pd_out[j] = pdate[j]
-            ncol[j] = cs.size
-            ngrp[j] = len(gw)
-            col[j, :cs.size] = cs
-            suf[j, :cs.size] = suffix[cs]
-            grp[j, :cs.size] = gs
-            gwa[j, :len(gw)] = gw
-        for sc in range(1, 5):
-            scol.extend(int(c) for c in cs if suffix[c] == sc)
-            soff.append(len(scol))
+    ncol = sel.sum(axis=1).astype(np.int32)
+    pd_out = np.where(ncol > 0, np.asarray(pdate), -1).astype(np.int32)
+    # selected entries in row-major order = each row's columns in column order
+    jj, cc = np.nonzero(sel)
+    kk = np.arange(jj.size) - np.concatenate([[0], np.cumsum(ncol)])[jj]
+    col[jj, kk] = cc
+    suf[jj, kk] = suffix[cc]
+    # prefix groups numbered by first appearance within the row
+    key = jj.astype(np.int64) * P + pid[cc]
+    uk, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")           # unique groups in (row, first position) order
+    urow = (uk // P)[order]
+    starts = np.flatnonzero(np.r_[True, urow[1:] != urow[:-1]]) if urow.size else np.zeros(0, np.int64)
+    run = np.repeat(starts, np.diff(np.r_[starts, urow.size]))
+    gnum = np.empty(uk.size, np.int64)
+    gnum[order] = np.arange(urow.size) - run
+    grp[jj, kk] = gnum[inv]
+    ngrp = np.bincount(uk // P, minlength=J).astype(np.int32) if uk.size else np.zeros(J, np.int32)
+    # group sums (composite_factor.py:281: pandas Series.sum = numpy sum over the members in
+    # column order: sequential from 0 below 8 members, numpy's pairwise sum from 8)
+    vals = W[jj, cc]
+    gsum = np.zeros(uk.size)
+    np.add.at(gsum, inv, vals)
+    big = np.flatnonzero(np.bincount(inv, minlength=uk.size) >= 8)
+    for u in big:
+        gsum[u] = vals[inv == u].sum()
+    tot = np.zeros(J)                                   # Python sum over groups in order (:282)
+    np.add.at(tot, urow, gsum[order])
+    r = uk // P
+    gw = np.where(tot[r] > 0, gsum / np.where(tot[r] > 0, tot[r], 1.0), 1.0 / np.maximum(ngrp[r], 1))
+    gwa[r, gnum] = gw
+    # pooled suffix column lists per (row, suffix 1..4), columns in column order (:251-268)
+    sc = suffix[cc]
+    m = (sc >= 1) & (sc <= 4)
+    idx = np.flatnonzero(m)
+    idx = idx[np.lexsort((kk[idx], sc[idx], jj[idx]))]
+    scol = cc[idx].astype(np.int32)
+    cnt = np.bincount(jj[m] * 4 + (sc[m] - 1), minlength=4 * J) if J else np.zeros(0, np.int64)
+    soff = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
     return {"pdate": pd_out, "ncol": ncol, "col": col, "suf": suf, "grp": grp, "ngrp": ngrp, "gw": gwa,
-            "KMAX": KMAX, "soff": np.asarray(soff, np.int32), "scol": np.asarray(scol or [0], np.int32)}
+            "KMAX": KMAX, "soff": soff, "scol": scol if scol.size else np.zeros(1, np.int32)}
 
 
 def _weighted_plan(P, selection_df: pd.DataFrame, used: list):
