@@ -30,6 +30,7 @@ constexpr int GK = 32;         // fp64 K chunk staged in LDS
 constexpr int GKP = GK + 2;    // padded row: bank = (4 r + 2 k) mod 64, conflict-free ds_read_b64
 constexpr int MK = 64;         // bf16 K chunk
 constexpr int MKP = MK + 8;    // padded row (16 B)
+constexpr size_t GRAM_F64_LDS = sizeof(double) * 2 * 2 * GT * GKP;   // k_gram_f64: 139 KB
 
 // Tile t of the row-major upper triangle of an nb x nb tile grid: (0,0), (0,1), ...,
 // (0,nb-1), (1,1), ...  (nb <= 16 at F = 2000, so the walk is short and block-uniform.)
@@ -118,12 +119,16 @@ __device__ __forceinline__ void load_chunk(const double* __restrict__ row, bool 
   }
 }
 
+// G = Z^T Z over one date slice, one 128 x 128 upper tile per workgroup: 8 waves as 2 x 4,
+// each a 64 x 32 sub-tile of 4 x 2 fp64 16x16x4 MFMAs.  K = (date, 32-asset chunk) pairs;
+// double-buffered LDS (2 x 2 x 128 x 34 doubles, dynamic): chunk c+1 is stored into the
+// other buffer after chunk c's MFMAs and chunk c+2's loads go out right behind the one
+// barrier per chunk, so the loads have a whole chunk of MFMAs to land.
 template <bool VEC>
 __global__ void __launch_bounds__(512)
 k_gram_f64(const double* __restrict__ Z, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
            int64_t dates_per_slice, int nb, int64_t ntile, double* __restrict__ part) {
-  __shared__ double As[GT * GKP];
-  __shared__ double Bs[GT * GKP];
+  extern __shared__ double gsm[];             // [2][As | Bs], GT * GKP doubles each
   const int64_t tile = blockIdx.x, slice = blockIdx.y;
   int ti, tj;
   upper_tile((int)tile, nb, ti, tj);
@@ -147,15 +152,24 @@ k_gram_f64(const double* __restrict__ Z, int64_t F, int64_t D, int64_t A, int64_
     load_chunk<VEC>(Z + ((int64_t)(i0 + lr) * D + d) * ld, rowA, a0, lc, A, ra);
     load_chunk<VEC>(Z + ((int64_t)(j0 + lr) * D + d) * ld, rowB, a0, lc, A, rb);
   };
-  if (total > 0) issue(0);
-  for (int64_t c = 0; c < total; ++c) {
+  auto stage = [&](int buf) {
+    double* As = gsm + buf * 2 * GT * GKP;
+    double* Bs = As + GT * GKP;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       As[lr * GKP + lc + u] = ra[u];
       Bs[lr * GKP + lc + u] = rb[u];
     }
-    __syncthreads();
-    if (c + 1 < total) issue(c + 1);   // next chunk in flight during the MFMAs
+  };
+  if (total > 0) {
+    issue(0);
+    stage(0);
+  }
+  __syncthreads();
+  if (total > 1) issue(1);
+  for (int64_t c = 0; c < total; ++c) {
+    const double* As = gsm + (c & 1) * 2 * GT * GKP;
+    const double* Bs = As + GT * GKP;
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
       const int k = kk + (lane >> 4);
@@ -170,7 +184,9 @@ k_gram_f64(const double* __restrict__ Z, int64_t F, int64_t D, int64_t A, int64_
         for (int n = 0; n < 2; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
     }
+    if (c + 1 < total) stage((int)((c + 1) & 1));   // that buffer was last read in chunk c-1
     __syncthreads();
+    if (c + 2 < total) issue(c + 2);
   }
   // C/D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
   double* p = part + (slice * ntile + tile) * (GT * GT);
@@ -214,46 +230,61 @@ k_gram_mask(const uint16_t* __restrict__ M, int64_t F, int64_t D, int64_t A, int
   const int lr = tid >> 1, lc = (tid & 1) * 32;
   const bool rowA = (i0 + lr) < F, rowB = (j0 + lr) < F;
   const bool vec = (ld % 8) == 0;   // 16-B aligned row segments
-  for (int64_t d = ds; d < de; ++d) {
+  // (date, 64-asset chunk) pairs flattened; the next chunk's loads are issued into
+  // registers before this chunk's MFMAs (single-buffered LDS, as k_gram_f64)
+  const int64_t nch = (A + MK - 1) / MK;
+  const int64_t total = (de - ds) * nch;
+  bf16x8 ra[4], rb[4];
+  auto issue = [&](int64_t c) {
+    const int64_t d = ds + c / nch, a0 = (c % nch) * MK;
     const uint16_t* ma = M + ((int64_t)(i0 + lr) * D + d) * ld;
     const uint16_t* mb = M + ((int64_t)(j0 + lr) * D + d) * ld;
-    for (int64_t a0 = 0; a0 < A; a0 += MK) {
-      if (vec && a0 + lc + 32 <= A) {
-        const bf16x8* pa = reinterpret_cast<const bf16x8*>(ma + a0 + lc);
-        const bf16x8* pb = reinterpret_cast<const bf16x8*>(mb + a0 + lc);
-        bf16x8 za = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 za = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (vec && a0 + lc + 32 <= A) {
+      const bf16x8* pa = reinterpret_cast<const bf16x8*>(ma + a0 + lc);
+      const bf16x8* pb = reinterpret_cast<const bf16x8*>(mb + a0 + lc);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          *reinterpret_cast<bf16x8*>(&As[lr * MKP + lc + 8 * u]) = rowA ? pa[u] : za;
-          *reinterpret_cast<bf16x8*>(&Bs[lr * MKP + lc + 8 * u]) = rowB ? pb[u] : za;
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 32; ++u) {
-          const int64_t a = a0 + lc + u;
-          As[lr * MKP + lc + u] = (rowA && a < A) ? ma[a] : (uint16_t)0;
-          Bs[lr * MKP + lc + u] = (rowB && a < A) ? mb[a] : (uint16_t)0;
-        }
+      for (int u = 0; u < 4; ++u) {
+        ra[u] = rowA ? pa[u] : za;
+        rb[u] = rowB ? pb[u] : za;
       }
-      __syncthreads();
+    } else {
 #pragma unroll
-      for (int ks = 0; ks < MK; ks += 16) {
-        const int k0 = ks + 8 * (lane >> 5);
-        bf16x8 af[2], bfr[2];
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
-          af[m] = *reinterpret_cast<const bf16x8*>(&As[(wr * 64 + m * 32 + (lane & 31)) * MKP + k0]);
+        for (int e = 0; e < 8; ++e) {
+          const int64_t a = a0 + lc + 8 * u + e;
+          ra[u][e] = (rowA && a < A) ? (short)ma[a] : (short)0;
+          rb[u][e] = (rowB && a < A) ? (short)mb[a] : (short)0;
+        }
+    }
+  };
+  if (total > 0) issue(0);
+  for (int64_t c = 0; c < total; ++c) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<bf16x8*>(&As[lr * MKP + lc + 8 * u]) = ra[u];
+      *reinterpret_cast<bf16x8*>(&Bs[lr * MKP + lc + 8 * u]) = rb[u];
+    }
+    __syncthreads();
+    if (c + 1 < total) issue(c + 1);
+#pragma unroll
+    for (int ks = 0; ks < MK; ks += 16) {
+      const int k0 = ks + 8 * (lane >> 5);
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        af[m] = *reinterpret_cast<const bf16x8*>(&As[(wr * 64 + m * 32 + (lane & 31)) * MKP + k0]);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bfr[n] = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + n * 32 + (lane & 31)) * MKP + k0]);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n)
-          bfr[n] = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + n * 32 + (lane & 31)) * MKP + k0]);
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
-      }
-      __syncthreads();
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
     }
+    __syncthreads();
   }
   double* p = part + (slice * ntile + tile) * (GT * GT);
 #pragma unroll
@@ -898,10 +929,12 @@ static fmx_status gram_run(const void* Zp, bool mask, double* G, int64_t F, int6
     k_gram_mask<<<grid, 256, 0, st>>>((const uint16_t*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_mask");
   } else if (ld % 2 == 0) {
-    k_gram_f64<true><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
+    FMX_HIP(hipFuncSetAttribute((const void*)k_gram_f64<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAM_F64_LDS));
+    k_gram_f64<true><<<grid, 512, GRAM_F64_LDS, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_f64");
   } else {
-    k_gram_f64<false><<<grid, 512, 0, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
+    FMX_HIP(hipFuncSetAttribute((const void*)k_gram_f64<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAM_F64_LDS));
+    k_gram_f64<false><<<grid, 512, GRAM_F64_LDS, st>>>((const double*)Zp, F, D, A, ld, d0, d1, pl.dps, pl.nb, pl.ntile, part);
     FMX_LAUNCH_CHECK("k_gram_f64");
   }
   k_gram_reduce<<<dim3((unsigned)pl.ntile, GT * GT / 256), 256, 0, st>>>(part, pl.nslice, pl.ntile, pl.nb, F, G,
