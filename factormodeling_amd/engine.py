@@ -435,14 +435,32 @@ def corr_prune_windows(X, stats, metrics, order, window: int, s0, use_rank_icir=
 def greedy_prune(C, order, rho=0.7, top_x=None):
     """Walk ``order``; keep f iff max |C[f, kept]| < rho (host, O(F * kept))."""
     Cn = C.detach().cpu().numpy() if isinstance(C, torch.Tensor) else np.asarray(C)
+    # f is kept iff max_k |C[f, k]| over the kept k is < rho or NaN (np.max propagates NaN
+    # and NaN >= rho is False).  Blocks of candidates: mx[g] = that max over the kept
+    # columns of earlier blocks (np.maximum propagates NaN too); inside a block the walk is
+    # sequential on the block's own |C| sub-matrix; then mx absorbs the block's kept columns.
+    mx = np.full(Cn.shape[0], -np.inf)
+    order = np.asarray(order, dtype=np.int64)
     kept = []
-    for f in order:
-        f = int(f)
-        if kept and np.max(np.abs(Cn[f, kept])) >= rho:
+    B = 64
+    for b0 in range(0, order.size, B):
+        cand = order[b0:b0 + B]
+        prior = mx[cand]
+        sub = np.abs(Cn[np.ix_(cand, cand)])
+        kin = []
+        bm = np.full(cand.size, -np.inf)     # max over this block's kept columns so far
+        for i in range(cand.size):
+            p, m = prior[i], bm[i]
+            if p == p and m == m and max(p, m) >= rho:
+                continue                     # (a NaN among the kept columns keeps it)
+            np.maximum(bm, sub[:, i], out=bm)
+            kin.append(i)
+            kept.append(int(cand[i]))
+            if top_x is not None and len(kept) >= top_x:
+                return kept
+        if not kin:
             continue
-        kept.append(f)
-        if top_x is not None and len(kept) >= top_x:
-            break
+        np.maximum(mx, np.abs(Cn[:, cand[kin]]).max(axis=1), out=mx)
     return kept
 
 
