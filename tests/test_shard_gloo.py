@@ -69,9 +69,11 @@ def _launch(world, skip_halo=False):
 
 
 @pytest.mark.timeout(600)
-def test_two_rank_step_matches_single_rank():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_step_matches_single_rank(world):
+    """2 ranks: one boundary; 3 ranks: a middle rank both receives and sends its halo."""
     from factormodeling_amd import pipeline as PL
-    res = _launch(2)
+    res = _launch(world)
     # single-rank reference (no process group needed for world == 1)
     cfg = PL.StepConfig(sel_window=W)
     sp = PL.ShardedPanel(D, A, F, 0, 1, torch.device("cpu"), seed=3)
