@@ -55,6 +55,11 @@ SIGNATURES = {
     "fmx_gram_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i32],
     "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     "fmx_gram_fused_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
+    "fmx_gram_exact": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
+    "fmx_gram_exact_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
+    "fmx_gram_exact_finalize": [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "fmx_gram_exact_units_per_date": [c_i64],
+    "fmx_debug_exact_fold": [c_vp, c_i64, c_vp, c_vp],
     "fmx_debug_pw_schedule": [c_i32, c_vp, c_i32],
     "fmx_comp_adj": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
     "fmx_comp_proxy": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp],
@@ -72,7 +77,8 @@ SIGNATURES = {
 }
 _RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
-             "fmx_cs_rank_sorted_work_bytes": c_i64}
+             "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
+             "fmx_debug_exact_fold": None}
 
 # constants mirrored from include/fmx.h
 TS = dict(sum=0, mean=1, std=2, var=3, zscore=4, rank=5, decay=6, diff=7, delay=8, backfill=9)

@@ -1,0 +1,193 @@
+"""Communication for the date-sharded step: the four exchanges ``pipeline.run_step`` makes
+between date shards, behind one small interface so the same step code runs over
+
+* ``TorchComm`` -- ``torch.distributed`` (RCCL over xGMI with backend "nccl" on the GPU
+  box; gloo on CPU): one process per GPU, the production path;
+* ``LocalComm`` -- N shards as N threads of ONE process on one device (tests): every
+  exchange is a device-to-device copy ordered by HIP events, so the whole sharded step
+  (halo send/recv, IC all-gather, exact Gram all-reduce) runs on the HIP kernels of a
+  single MI355X and can be compared bit-for-bit with the 1-shard run.
+
+Exchanges: point-to-point halo slabs to rank+1 (``isend``/``irecv``),
+the daily IC series (``all_gather``) and the exact Gram limbs / pair counts
+(``all_reduce_sum`` of int64 -- integer sums, so the reduction order is free).
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+import torch.distributed as dist
+
+
+class TorchComm:
+    """torch.distributed on the default process group (RCCL / gloo)."""
+
+    def __init__(self):
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+
+    def isend(self, t, dst):
+        return dist.isend(t, dst)
+
+    def irecv(self, t, src):
+        return dist.irecv(t, src)
+
+    def all_gather(self, t):
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t.contiguous())
+        return parts
+
+    def all_reduce_sum(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def barrier(self):
+        dist.barrier()
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _Recv:
+    def __init__(self, hub, key, out):
+        self.hub, self.key, self.out = hub, key, out
+
+    def wait(self):
+        t, ev = self.hub.take(self.key)
+        if ev is not None:
+            st = torch.cuda.current_stream(self.out.device)
+            st.wait_event(ev)
+            t.record_stream(st)                  # allocated on the sender's stream
+        self.out.copy_(t)
+
+
+class LocalHub:
+    """Rendezvous of ``world`` in-process shards (one thread each)."""
+
+    def __init__(self, world, timeout=300.0):
+        self.world = world
+        self.timeout = timeout
+        self._cv = threading.Condition()
+        self._mail = {}
+        self._barrier = threading.Barrier(world, timeout=timeout)
+        self._slots = [None] * world
+        self.failed = False
+
+    def abort(self):
+        """A shard failed: wake every waiter (they raise instead of timing out)."""
+        with self._cv:
+            self.failed = True
+            self._cv.notify_all()
+        self._barrier.abort()
+
+    def post(self, key, t):
+        ev = None
+        if t.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(t.device))
+        with self._cv:
+            self._mail.setdefault(key, []).append((t, ev))
+            self._cv.notify_all()
+
+    def take(self, key):
+        with self._cv:
+            ok = self._cv.wait_for(lambda: self.failed or self._mail.get(key), timeout=self.timeout)
+            if self.failed:
+                raise RuntimeError("LocalComm: another shard failed")
+            if not ok:
+                raise TimeoutError(f"LocalComm: no message for {key}")
+            return self._mail[key].pop(0)
+
+    def gather(self, rank, t):
+        """Every rank's ``t`` (a private copy made on the caller's stream), rank order."""
+        c = t.clone()
+        ev = None
+        if c.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(c.device))
+        self._barrier.wait()                      # previous gather fully consumed
+        self._slots[rank] = (c, ev)
+        self._barrier.wait()                      # all deposited
+        got = list(self._slots)
+        self._barrier.wait()                      # all read the slot list
+        out = []
+        for x, e in got:
+            if e is not None:
+                st = torch.cuda.current_stream(x.device)
+                st.wait_event(e)
+                x.record_stream(st)              # allocated on the depositor's stream
+            out.append(x.clone())                  # own copy, ordered after the producer
+        return out
+
+
+class LocalComm:
+    """One shard's endpoint on a LocalHub (same interface as TorchComm)."""
+
+    def __init__(self, hub: LocalHub, rank: int):
+        self.hub, self.rank, self.world = hub, rank, hub.world
+        self._n = {}
+
+    def _key(self, src, dst):
+        k = (src, dst)
+        self._n[k] = self._n.get(k, 0) + 1
+        return (src, dst, self._n[k])
+
+    def isend(self, t, dst):
+        self.hub.post(self._key(self.rank, dst), t.clone())
+        return _Done()
+
+    def irecv(self, t, src):
+        return _Recv(self.hub, self._key(src, self.rank), t)
+
+    def all_gather(self, t):
+        return self.hub.gather(self.rank, t.contiguous())
+
+    def all_reduce_sum(self, t):
+        parts = self.hub.gather(self.rank, t.contiguous())
+        acc = parts[0]
+        for p in parts[1:]:
+            acc += p
+        t.copy_(acc)
+        return t
+
+    def barrier(self):
+        self.hub._barrier.wait()
+
+
+def run_local_shards(world, fn, timeout=600.0):
+    """Run ``fn(rank, comm)`` for ``world`` in-process shards on threads; each thread runs
+    on its own HIP stream when a GPU is present.  Returns the per-rank results and re-raises
+    the first shard's exception."""
+    hub = LocalHub(world, timeout=timeout)
+    res = [None] * world
+    err = [None] * world
+
+    def body(r):
+        try:
+            if torch.cuda.is_available():
+                with torch.cuda.stream(torch.cuda.Stream()):
+                    res[r] = fn(r, LocalComm(hub, r))
+                    torch.cuda.current_stream().synchronize()
+            else:
+                res[r] = fn(r, LocalComm(hub, r))
+        except BaseException as e:  # noqa: BLE001 -- reported to the caller below
+            err[r] = e
+            hub.abort()
+
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    for e in err:      # the original failure, not the other shards' aborted waits
+        if e is not None and not isinstance(e, threading.BrokenBarrierError) and "another shard" not in str(e):
+            raise e
+    for e in err:
+        if e is not None:
+            raise e
+    if any(t.is_alive() for t in th):
+        raise TimeoutError("LocalComm shards did not finish")
+    return res

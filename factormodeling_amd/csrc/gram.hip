@@ -16,9 +16,12 @@
 
 #include <cstdlib>
 
+#include "exactsum.hpp"
 #include "rowkit.hpp"
 
 namespace fmx {
+
+static_assert(EX_SLOTS == FMX_GRAM_EXACT_SLOTS, "exact Gram limb layout");
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef float flt16 __attribute__((ext_vector_type(16)));
@@ -470,11 +473,23 @@ k_gram_small(const double* __restrict__ X, const double* __restrict__ stats, int
 // waves' MFMAs), issues the loads of chunk c+2, runs chunk c's MFMAs, then one barrier.
 // Slices are equal ranges of the flattened (date, 32-asset block) chunk sequence, one per
 // CU.  The row stats are double-buffered by date parity, loaded one date ahead.
-template <int NB, bool ZIN>   // ZIN: X already holds the z-scores (cs_zscore output), stats unused
+//
+// UNITS (the exact, GPU-count-independent Gram, fmx_gram_exact): the K range is cut into
+// fixed units -- unit u = part u % S of date u / S, i.e. asset chunks [(u%S) nch / S,
+// (u%S + 1) nch / S) of that date -- and each workgroup walks an equal range of units,
+// writing its accumulators to part[unit][NTRI][256] at every unit boundary (dbl4 per lane,
+// C-map order) and restarting them.  A unit's partial depends only on its own (date, asset
+// range), never on the launch's date range or the CU count, so the exact fold of the
+// partials (k_gram_fold) gives the same G however the dates are split over GPUs.
+__host__ __device__ inline int64_t unit_chunk(int64_t u, int S, int64_t nch) {
+  return (u / S) * nch + ((u % S) * nch) / S;
+}
+
+template <int NB, bool ZIN, bool UNITS = false>   // ZIN: X holds the z-scores (cs_zscore output), stats unused
 __global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
           int64_t ld, int64_t d0, int64_t nch, int64_t total, int64_t nslice, double* __restrict__ part,
-          uint32_t* __restrict__ mbits, int opt) {
+          uint32_t* __restrict__ mbits, int opt, int units_per_date = 1) {
   constexpr int FP = 16 * NB;
   constexpr int NTRI = NB * (NB + 1) / 2;
   constexpr int NWV = SG_NT / 64;
@@ -485,7 +500,11 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   __shared__ double mu_s[2][FP], sd_s[2][FP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t slice = blockIdx.x;
-  const int64_t c0 = slice * total / nslice, c1 = (slice + 1) * total / nslice;
+  // UNITS: ``total`` counts units; the slice's chunk range is its units' (contiguous) chunks
+  const int S = units_per_date;
+  const int64_t u0 = slice * total / nslice, u1 = (slice + 1) * total / nslice;
+  const int64_t c0 = UNITS ? unit_chunk(u0, S, nch) : u0, c1 = UNITS ? unit_chunk(u1, S, nch) : u1;
+  int64_t cur_u = u0, u_end = UNITS ? unit_chunk(u0 + 1, S, nch) : 0;
   int blk[BPW];
 #pragma unroll
   for (int u = 0; u < BPW; ++u) {
@@ -581,9 +600,23 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
         gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
       }
     }
+    if (UNITS) {
+      while (c + 1 == u_end) {                    // unit cur_u complete (empty units: zeros)
+        double* pu = part + (cur_u * NTRI) * 256 + lane * 4;
+#pragma unroll
+        for (int u = 0; u < BPW; ++u) {
+          if (blk[u] < 0) continue;
+          *reinterpret_cast<dbl4*>(pu + (int64_t)(wid + NWV * u) * 256) = gacc[u];
+          gacc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+        }
+        if (++cur_u >= u1) break;
+        u_end = unit_chunk(cur_u + 1, S, nch);
+      }
+    }
     if (mfma_first) next();
     __syncthreads();
   }
+  if (UNITS) return;
   double* p = part + slice * (int64_t)FP * FP;
 #pragma unroll
   for (int u = 0; u < BPW; ++u) {
@@ -620,6 +653,62 @@ __global__ void k_gram_small_reduce(const double* __restrict__ partG, const doub
   G[(int64_t)j * F + i] = g;
   N[(int64_t)i * F + j] = n;
   N[(int64_t)j * F + i] = n;
+}
+
+// Exact fold of k_gram_db<.,.,true>'s unit partials part[unit][NTRI][256] into the
+// fixed-point limbs [EX_SLOTS][F][F] (upper triangle incl. the diagonal), and of the
+// popcount pair counts into counts[F][F].  grid = (NTRI triangle blocks, unit groups) x
+// 256 threads; thread e = element e of the block in the fp64 16x16x4 C map (lane e >> 2,
+// register e & 3).  Each thread folds its group's units in registers, then adds its limbs
+// with 64-bit integer atomics: integer addition, so neither the unit grouping nor the
+// atomics' arrival order changes a bit of the result.
+__global__ void __launch_bounds__(256)
+k_gram_fold(const double* __restrict__ part, int64_t nunits, int64_t upg, int NB, int64_t F,
+            int64_t* __restrict__ limbs, const unsigned long long* __restrict__ ncnt, int FP,
+            int64_t* __restrict__ counts) {
+  const int ntri = NB * (NB + 1) / 2;
+  int t = blockIdx.x, bi = 0;
+  while (t >= NB - bi) { t -= NB - bi; ++bi; }
+  const int bj = bi + t;
+  const int e = threadIdx.x, lane = e >> 2, r = e & 3;
+  const int64_t row = bi * 16 + (lane >> 4) + 4 * r, col = bj * 16 + (lane & 15);
+  if (row >= F || col >= F || row > col) return;
+  int64_t acc[EX_SLOTS];
+#pragma unroll
+  for (int k = 0; k < EX_SLOTS; ++k) acc[k] = 0;
+  const int64_t ua = (int64_t)blockIdx.y * upg, ub = min<int64_t>(nunits, ua + upg);
+  const double* p = part + (int64_t)blockIdx.x * 256 + e;
+#pragma unroll 4
+  for (int64_t u = ua; u < ub; ++u) ex_add(acc, p[u * ntri * 256]);
+  const int64_t FF = F * F, o = row * F + col;
+#pragma unroll
+  for (int k = 0; k < EX_SLOTS; ++k)
+    if (acc[k]) atomicAdd(reinterpret_cast<unsigned long long*>(limbs + k * FF + o), (unsigned long long)acc[k]);
+  if (blockIdx.y == 0 && ncnt) {
+    const unsigned long long n = ncnt[row * FP + col];
+    if (n) atomicAdd(reinterpret_cast<unsigned long long*>(counts + o), n);
+  }
+}
+
+// G, N [F][F] (symmetric) from the (all-reduced) limbs and counts.
+__global__ void __launch_bounds__(256)
+k_gram_finalize(const int64_t* __restrict__ limbs, const int64_t* __restrict__ counts, int64_t F,
+                double* __restrict__ G, double* __restrict__ N) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, FF = F * F;
+  if (e >= FF) return;
+  const int64_t i = e / F, j = e % F;
+  if (i > j) return;
+  int64_t acc[EX_SLOTS];
+#pragma unroll
+  for (int k = 0; k < EX_SLOTS; ++k) acc[k] = limbs[k * FF + e];
+  const double g = ex_value(acc);
+  G[e] = g;
+  G[j * F + i] = g;
+  if (N) {
+    const double n = (double)counts[e];
+    N[e] = n;
+    N[j * F + i] = n;
+  }
 }
 
 // N = M M^T from the validity bits k_gram_small<.,0> packed (32 assets per word, stored
@@ -755,6 +844,78 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
   k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(
       part, mask_mfma ? part + st_elems : nullptr, nslice, FP, F, G, N, accumulate, mask_mfma ? nullptr : ncnt);
   FMX_LAUNCH_CHECK("k_gram_small_reduce");
+  return FMX_OK;
+}
+
+// Workspace of the exact Gram (fmx_gram_exact): unit partials, validity bits, pair counts.
+// Units per date depend on A only (2560-asset halves of a 5,000-asset row), never on the
+// date range or the device, so every GPU count folds the same partials.
+struct ExactPlan {
+  int64_t FP, ntri, nch, S, nunits, nw, F;
+  int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * nunits * ntri * 256); }
+  int64_t bits_bytes() const { return SmallPlan::align256((int64_t)sizeof(uint32_t) * nw * F); }
+  int64_t cnt_bytes() const { return (int64_t)sizeof(unsigned long long) * FP * FP; }
+  int64_t bytes() const { return part_bytes() + bits_bytes() + cnt_bytes(); }
+};
+static int64_t exact_units_per_date(int64_t A) {
+  const int64_t nch = std::max<int64_t>(1, ceil_div(A, (int64_t)SG_K));
+  return std::min<int64_t>(nch, std::max<int64_t>(1, ceil_div(A, 2560)));
+}
+static ExactPlan exact_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
+  ExactPlan p;
+  const int64_t nb = ceil_div(std::max<int64_t>(F, 1), 16);
+  p.F = F;
+  p.FP = 16 * nb;
+  p.ntri = nb * (nb + 1) / 2;
+  p.nch = ceil_div(A, (int64_t)SG_K);
+  p.S = exact_units_per_date(A);
+  p.nunits = std::max<int64_t>(d1 - d0, 0) * p.S;
+  p.nw = std::max<int64_t>(d1 - d0, 0) * p.nch;
+  return p;
+}
+
+template <int NB>
+static fmx_status gram_exact_launch(const double* X, const double* stats, int64_t* limbs, int64_t* counts, int64_t F,
+                                    int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, char* work,
+                                    hipStream_t st) {
+  constexpr int FP = 16 * NB;
+  const ExactPlan pl = exact_plan(F, A, d0, d1);
+  if (pl.nunits == 0 || A == 0) return FMX_OK;
+  FMX_ARG(pl.nw * F < ((int64_t)1 << 32), "panel too large for 32-bit validity-word indices");
+  double* part = reinterpret_cast<double*>(work);
+  uint32_t* mbits = reinterpret_cast<uint32_t*>(work + pl.part_bytes());
+  unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(work + pl.part_bytes() + pl.bits_bytes());
+  FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return std::max(n, 1);
+  }();
+  const int64_t nslice = std::max<int64_t>(1, std::min<int64_t>(pl.nunits, cus));
+  static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
+  if (stats)
+    k_gram_db<NB, false, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
+                                                                    nslice, part, mbits, gopt, (int)pl.S);
+  else
+    k_gram_db<NB, true, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
+                                                                   nslice, part, mbits, gopt, (int)pl.S);
+  FMX_LAUNCH_CHECK("k_gram_db<units>");
+  {
+    const int T = (int)ceil_div(F, (int64_t)32);
+    const int ntile = T * (T + 1) / 2;
+    const int64_t nw = pl.nw;
+    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PC_W), 2048 / ntile + 1));
+    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PC_W) * PC_W;
+    const unsigned nky = (unsigned)ceil_div(nw, wps);
+    k_gram_popc<<<dim3((unsigned)ntile, nky), 256, 0, st>>>(mbits, F, nw, wps, FP, ncnt);
+    FMX_LAUNCH_CHECK("k_gram_popc");
+  }
+  const int64_t ngroups = std::max<int64_t>(1, std::min<int64_t>(pl.nunits, 2048 / pl.ntri));
+  const int64_t upg = ceil_div(pl.nunits, ngroups);
+  k_gram_fold<<<dim3((unsigned)pl.ntri, (unsigned)ceil_div(pl.nunits, upg)), 256, 0, st>>>(
+      part, pl.nunits, upg, NB, F, limbs, ncnt, FP, counts);
+  FMX_LAUNCH_CHECK("k_gram_fold");
   return FMX_OK;
 }
 
@@ -897,6 +1058,62 @@ extern "C" fmx_status fmx_gram_fused(const double* X, const double* stats, doubl
 #undef FMX_GS
     default: return FMX_ERR_UNSUPPORTED;
   }
+}
+
+extern "C" int64_t fmx_gram_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
+  (void)D;
+  if (F <= 0 || F > 256 || d1 <= d0 || A <= 0) return 0;
+  return exact_plan(F, A, d0, d1).bytes();
+}
+
+extern "C" fmx_status fmx_gram_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts,
+                                     int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
+                                     int32_t accumulate, void* work, int64_t work_bytes, void* stream) {
+  FMX_ARG(X && limbs && counts, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
+  if (F > 256) {
+    set_error("fmx_gram_exact supports F <= 256");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  hipStream_t st = as_stream(stream);
+  if (!accumulate && F > 0) {
+    FMX_HIP(hipMemsetAsync(limbs, 0, sizeof(int64_t) * FMX_GRAM_EXACT_SLOTS * F * F, st));
+    FMX_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * F * F, st));
+  }
+  if (F == 0 || d1 == d0 || A == 0) return FMX_OK;
+  if (fmx_status e = check_work(work, work_bytes, fmx_gram_exact_work_bytes(F, D, A, d0, d1),
+                                "fmx_gram_exact_work_bytes"))
+    return e;
+  char* w = static_cast<char*>(work);
+  switch ((int)ceil_div(F, 16)) {
+#define FMX_GE(K) \
+  case K: return gram_exact_launch<K>(X, stats, limbs, counts, F, D, A, ld, d0, d1, w, st);
+    FMX_GE(1) FMX_GE(2) FMX_GE(3) FMX_GE(4) FMX_GE(5) FMX_GE(6) FMX_GE(7) FMX_GE(8)
+    FMX_GE(9) FMX_GE(10) FMX_GE(11) FMX_GE(12) FMX_GE(13) FMX_GE(14) FMX_GE(15) FMX_GE(16)
+#undef FMX_GE
+    default: return FMX_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" fmx_status fmx_gram_exact_finalize(const int64_t* limbs, const int64_t* counts, double* G, double* N,
+                                              int64_t F, void* stream) {
+  FMX_ARG(limbs && G && (counts || !N), "null pointer");
+  FMX_ARG(F >= 0, "bad dims");
+  if (F == 0) return FMX_OK;
+  k_gram_finalize<<<(unsigned)ceil_div(F * F, 256), 256, 0, as_stream(stream)>>>(limbs, counts, F, G, N);
+  FMX_LAUNCH_CHECK("k_gram_finalize");
+  return FMX_OK;
+}
+
+extern "C" int32_t fmx_gram_exact_units_per_date(int64_t A) { return (int32_t)exact_units_per_date(A); }
+
+// Host run of the device's exact accumulator (exactsum.hpp is __host__ __device__): the CPU
+// tests pin it against the numpy restatement without a GPU.
+extern "C" void fmx_debug_exact_fold(const double* x, int64_t n, int64_t* limbs_out, double* value_out) {
+  int64_t acc[EX_SLOTS] = {0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = 0; i < n; ++i) ex_add(acc, x[i]);
+  for (int k = 0; k < EX_SLOTS; ++k) limbs_out[k] = acc[k];
+  if (value_out) *value_out = ex_value(acc);
 }
 
 extern "C" fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,

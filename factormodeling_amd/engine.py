@@ -367,6 +367,46 @@ def gram_fused(X, stats, d0=0, d1=None):
     return G, N
 
 
+GRAM_EXACT_SLOTS = 7            # fmx.h FMX_GRAM_EXACT_SLOTS: 6 payload limbs + flag
+
+
+def gram_exact(X, stats=None, d0=0, d1=None, limbs=None, counts=None, accumulate=False):
+    """Exact fixed-point Gram partials over dates [d0, d1) (fmx_gram_exact, F <= 256):
+    (limbs int64 [7][F][F], counts int64 [F][F]), upper triangles.  Integer sums: ranks
+    add them with any all-reduce and gram_exact_finalize gives the same G / N bits at every
+    GPU count.  ``stats=None``: X holds the z-scores (the step's cs_zscore output)."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if F > FUSED_GRAM_MAX_F:
+        raise _lib.FmxError("gram_exact: F <= 256")
+    if stats is not None and (tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous()):
+        raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
+    d1 = D if d1 is None else d1
+    if limbs is None:
+        limbs = torch.empty((GRAM_EXACT_SLOTS, F, F), dtype=torch.int64, device=X.device)
+    if counts is None:
+        counts = torch.empty((F, F), dtype=torch.int64, device=X.device)
+    if tuple(limbs.shape) != (GRAM_EXACT_SLOTS, F, F) or limbs.dtype != torch.int64 or not limbs.is_contiguous() \
+            or tuple(counts.shape) != (F, F) or counts.dtype != torch.int64 or not counts.is_contiguous():
+        raise _lib.FmxError("gram_exact: limbs int64 [7][F][F], counts int64 [F][F]")
+    nb = int(_lib.load().fmx_gram_exact_work_bytes(F, D, A, int(d0), int(d1)))
+    work, wb = _workspace_bytes(X.device, nb)
+    call("fmx_gram_exact", ptr(X), ptr(stats), ptr(limbs), ptr(counts), F, D, A, A, int(d0), int(d1),
+         int(bool(accumulate)), ptr(work), wb, stream_ptr())
+    return limbs, counts
+
+
+def gram_exact_finalize(limbs, counts):
+    """G, N [F][F] float64 (symmetric) from (all-reduced) exact limbs / counts."""
+    F = limbs.shape[1]
+    G = torch.empty((F, F), dtype=F64, device=limbs.device)
+    N = torch.empty((F, F), dtype=F64, device=limbs.device)
+    call("fmx_gram_exact_finalize", ptr(limbs.contiguous()), ptr(counts.contiguous()), ptr(G), ptr(N), F,
+         stream_ptr())
+    return G, N
+
+
 GRAM_CHUNK_BYTES = 8 << 30      # Z + M workspace of one date chunk of the wide Gram
 
 

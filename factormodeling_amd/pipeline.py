@@ -24,7 +24,6 @@ import os
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from . import engine as E
 
@@ -160,17 +159,46 @@ def synthetic_panel(D, A, F, device, seed=0, d_lo=0, d_hi=None, halo=0):
     return X, R, lo
 
 
+def shard_bounds(D, world, rank):
+    """Owned dates [d_lo, d_hi) of ``rank``: contiguous blocks of ceil(D / world) dates."""
+    per = (D + world - 1) // world
+    return min(D, rank * per), min(D, (rank + 1) * per)
+
+
+def check_sharding(D, world, halo):
+    """Every rank must own at least one date, and every rank that sends a halo (all but the
+    last) at least ``halo`` dates: its last ``halo`` rows are the next rank's warm-up, and
+    with fewer they would include its own not-yet-received halo rows."""
+    for r in range(world):
+        lo, hi = shard_bounds(D, world, r)
+        if hi - lo < 1 or (r + 1 < world and hi - lo < halo):
+            raise ValueError(f"date sharding of D={D} over {world} ranks: rank {r} owns {hi - lo} dates, "
+                             f"needs >= {max(1, halo) if r + 1 < world else 1} (halo {halo})")
+
+
 class ShardedPanel:
     """A rank's slice of the date axis: owned dates [d_lo, d_hi) plus ``halo`` preceding
-    dates, stored contiguously as X[F][halo + own][A]."""
+    dates, stored contiguously as X[F][halo + own][A].  ``comm`` carries the exchanges
+    (factormodeling_amd.comm: TorchComm over RCCL / gloo, or LocalComm for in-process
+    shards); by default torch.distributed's process group when one is initialised."""
 
-    def __init__(self, D, A, F, rank, world, device, seed=0, halo=HALO):
+    def __init__(self, D, A, F, rank=None, world=None, device=None, seed=0, halo=HALO, comm=None):
         # halo: rolling warm-up + IC lag of the step's longest window (StepConfig.halo)
+        if comm is None and world is not None and world > 1:
+            from .comm import TorchComm
+            comm = TorchComm()
+        if comm is not None:
+            rank = comm.rank if rank is None else rank
+            world = comm.world if world is None else world
+            if (rank, world) != (comm.rank, comm.world):
+                raise ValueError("rank / world disagree with the comm")
+        rank = 0 if rank is None else rank
+        world = 1 if world is None else world
+        self.comm = comm
         self.D, self.A, self.F = D, A, F
         self.rank, self.world = rank, world
-        per = (D + world - 1) // world
-        self.d_lo = min(D, rank * per)
-        self.d_hi = min(D, (rank + 1) * per)
+        check_sharding(D, world, halo)
+        self.d_lo, self.d_hi = shard_bounds(D, world, rank)
         self.halo = halo if rank > 0 else 0
         self.halo_len = halo
         self.device = device
@@ -190,9 +218,9 @@ class ShardedPanel:
 
     def exchange_halo_start(self):
         """Post the halo exchange: send my last ``halo`` owned dates to rank+1, receive
-        rank-1's (RCCL point-to-point over xGMI; gloo on CPU).  Asynchronous: work that
-        needs no halo row runs while the transfer is in flight; exchange_halo_finish()
-        waits and writes the received rows into the halo."""
+        rank-1's (RCCL point-to-point over xGMI; gloo on CPU; device copies in-process).
+        Asynchronous: work that needs no halo row runs while the transfer is in flight;
+        exchange_halo_finish() waits and writes the received rows into the halo."""
         if self.world == 1:
             return None
         H = self.halo_len
@@ -201,14 +229,14 @@ class ShardedPanel:
             send_x = self.X[:, -H:].contiguous()
             send_r = self.R[-H:].contiguous()
             bufs += [send_x, send_r]
-            reqs.append(dist.isend(send_x, self.rank + 1))
-            reqs.append(dist.isend(send_r, self.rank + 1))
+            reqs.append(self.comm.isend(send_x, self.rank + 1))
+            reqs.append(self.comm.isend(send_r, self.rank + 1))
         recv = None
         if self.rank > 0:
             recv = (torch.empty((self.F, self.halo, self.A), dtype=self.X.dtype, device=self.X.device),
                     torch.empty((self.halo, self.A), dtype=self.R.dtype, device=self.R.device))
-            reqs.append(dist.irecv(recv[0], self.rank - 1))
-            reqs.append(dist.irecv(recv[1], self.rank - 1))
+            reqs.append(self.comm.irecv(recv[0], self.rank - 1))
+            reqs.append(self.comm.irecv(recv[1], self.rank - 1))
         return reqs, recv, bufs
 
     def exchange_halo_finish(self, handle):
@@ -277,11 +305,25 @@ class EngineBackend:
         return E.cs_moment_stats("zscore", X, out=out)
 
     @staticmethod
+    def corr_gram_exact(X, d0, d1, stats=None, z=None):
+        """Exact fixed-point Gram partials over dates [d0, d1) (F <= 256): from ``z``, the
+        step's cs_zscore output, when given, else from X with the row stats."""
+        if z is not None:
+            return E.gram_exact(z, None, d0, d1)
+        if stats is None:
+            _, stats = E.cs_moment_stats("stats", X)
+        return E.gram_exact(X, stats, d0, d1)
+
+    gram_exact_finalize = staticmethod(E.gram_exact_finalize)
+
+    @staticmethod
     def corr_gram(X, d0, d1, stats=None, z=None):
         """G, N over dates [d0, d1): fused single pass for F <= 256 (from ``z``, the
         step's cs_zscore output, when given), else Z/M + tiles."""
         if X.shape[0] <= E.FUSED_GRAM_MAX_F:
-            if z is not None:
+            # the z input needs the default kernel; the A/B switches take the stats path
+            ab = os.environ.get("FMX_GRAM_SINGLE_BUFFER") or os.environ.get("FMX_GRAM_MASK_MFMA")
+            if z is not None and not ab:
                 return E.gram_fused(z, None, d0, d1)
             if stats is None:
                 _, stats = E.cs_moment_stats("stats", X)
@@ -444,7 +486,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
                               own=slice(sp.halo, None), side=side, only=lambda n: n == "cs_zscore_neutralize")
         if cfg.gram and hasattr(be, "corr_gram"):
             t0 = _ev(timers)
-            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
+            GN = gram_partials(sp, be, side)
             _rec(timers, "gram", t0)
     t0 = _ev(timers)
     sp.exchange_halo_finish(halo)
@@ -465,7 +507,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)
-            GN = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
+            GN = gram_partials(sp, be, side)
             _rec(timers, "gram", t0)
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
@@ -494,8 +536,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         per = (sp.D + sp.world - 1) // sp.world
         pad = torch.zeros((L, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
         pad[..., :daily.shape[3]] = daily
-        parts = [torch.empty_like(pad) for _ in range(sp.world)]
-        dist.all_gather(parts, pad)
+        parts = sp.comm.all_gather(pad)
         full = torch.cat(parts, dim=3)[:, :, :, :sp.D].contiguous()
     else:
         full = daily.contiguous()
@@ -524,16 +565,12 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         # correlation Gram over owned dates, summed over ranks in rank order
         t0 = _ev(timers)
         if GN is not None:
-            G, N = GN                             # made on streams[1]: now used on this one
-            G.record_stream(torch.cuda.current_stream(G.device))
-            N.record_stream(torch.cuda.current_stream(N.device))
-        elif hasattr(be, "corr_gram"):
-            G, N = be.corr_gram(sp.X, sp.halo, sp.X.shape[1], side.get("stats"), side.get("zscore"))
+            for T in GN[1]:                       # made on streams[1]: now used on this one
+                if T.is_cuda:
+                    T.record_stream(torch.cuda.current_stream(T.device))
         else:
-            Z, M = be.zscore_exposures(sp.X[:, sp.halo:].contiguous())
-            G, N = be.gram(Z, M)
-        if sp.world > 1:
-            G, N = ordered_sum(G, sp.world), ordered_sum(N, sp.world)
+            GN = gram_partials(sp, be, side)
+        G, N = gram_total(sp, be, GN)
         C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
         _rec(timers, "gram_sum" if GN is not None else "gram", t0)
         t0 = _ev(timers)
@@ -545,6 +582,35 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if collect is not None:
         collect.update(daily=full, summ=summ, win=win, C=C, comp=comp)
     return w, kept
+
+
+def gram_partials(sp, be, side):
+    """This rank's share of the factor Gram over its owned dates: ("exact", (limbs, counts))
+    -- integer fixed-point partials whose sum over ranks is independent of the GPU count
+    (F <= 256, gram_exact) -- or ("float", (G, N)) for the wide chunked path."""
+    d0, d1 = sp.halo, sp.X.shape[1]
+    if hasattr(be, "corr_gram_exact") and sp.F <= E.FUSED_GRAM_MAX_F:
+        return "exact", be.corr_gram_exact(sp.X, d0, d1, side.get("stats"), side.get("zscore"))
+    if hasattr(be, "corr_gram"):
+        return "float", be.corr_gram(sp.X, d0, d1, side.get("stats"), side.get("zscore"))
+    Z, M = be.zscore_exposures(sp.X[:, d0:].contiguous())
+    return "float", be.gram(Z, M)
+
+
+def gram_total(sp, be, part):
+    """G, N over all ranks' dates.  Exact partials: int64 all-reduce (RCCL over xGMI; the
+    integer sum is the same in any order) then finalize -- the same bits at 1, 2, 4 or 8
+    GPUs, so the kept set never depends on the GPU count.  Float partials: rank-ordered sum
+    (identical on every rank of one run)."""
+    kind, (a, b) = part
+    if kind == "exact":
+        if sp.world > 1:
+            sp.comm.all_reduce_sum(a)
+            sp.comm.all_reduce_sum(b)
+        return be.gram_exact_finalize(a, b)
+    if sp.world > 1:
+        a, b = ordered_sum(a, sp.comm), ordered_sum(b, sp.comm)
+    return a, b
 
 
 def weighted_composite_step(sp, cfg, w, be=ENGINE):
@@ -563,12 +629,11 @@ def weighted_composite_step(sp, cfg, w, be=ENGINE):
     return be.wcomp(sp.X, plan, cfg.composite)
 
 
-def ordered_sum(T, world):
-    """Sum of every rank's ``T`` in rank order (all-gather + sequential adds), so the Gram
-    that feeds the discrete pruning decision is bitwise identical on every rank and from
-    run to run (an RCCL all-reduce leaves the summation order to the ring/tree)."""
-    parts = [torch.empty_like(T) for _ in range(world)]
-    dist.all_gather(parts, T.contiguous())
+def ordered_sum(T, comm):
+    """Sum of every rank's ``T`` in rank order (all-gather + sequential adds): identical on
+    every rank, but a different rounding of the sum at each GPU count.  Only the wide (F >
+    256) Gram still uses it; F <= 256 goes through the exact limbs (gram_exact)."""
+    parts = comm.all_gather(T.contiguous())
     acc = parts[0].clone()
     for p in parts[1:]:
         acc += p

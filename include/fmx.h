@@ -243,6 +243,28 @@ fmx_status fmx_gram_fused(const double* X, const double* stats, double* G, doubl
                           int64_t work_bytes, void* stream);
 /* Device workspace fmx_gram_fused needs (per-slice partial tiles, validity bits, counts). */
 int64_t fmx_gram_fused_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1);
+/* Exact, GPU-count-independent form of fmx_gram_fused (F <= 256) for the date-sharded
+ * step (SURVEY 5 "bit-identical at 1/2/4/8 GPUs"; replaces the float sum of Gram partials
+ * behind the builder-defined corr-prune, A19).  The dates [d0, d1) are cut into fixed
+ * units (fmx_gram_exact_units_per_date(A) asset ranges per date), each unit's Z^T Z is
+ * computed on fp64 MFMA and folded into a signed fixed-point accumulator (LSB 2^-64, 6 x
+ * 32-bit payload limbs in int64 + an invalid-term flag): limbs [FMX_GRAM_EXACT_SLOTS][F][F]
+ * (upper triangle), counts [F][F] int64 pair counts (upper triangle).  Both are plain
+ * integer sums, so ranks add them with an int64 all-reduce (any order) and
+ * fmx_gram_exact_finalize gives the same G and N bits at every GPU count.  accumulate = 0
+ * zeroes limbs and counts first.  stats == NULL: X holds the z-scores (as fmx_gram_fused). */
+#define FMX_GRAM_EXACT_SLOTS 7
+fmx_status fmx_gram_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts, int64_t F,
+                          int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,
+                          int64_t work_bytes, void* stream);
+int64_t fmx_gram_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1);
+/* G, N [F][F] (symmetric) from exact limbs / counts (N and counts may be NULL); a flagged
+ * (non-finite or >= 2^127) term makes the entry NaN. */
+fmx_status fmx_gram_exact_finalize(const int64_t* limbs, const int64_t* counts, double* G, double* N, int64_t F,
+                                   void* stream);
+int32_t fmx_gram_exact_units_per_date(int64_t A);
+/* Host-side run of the same accumulator over n doubles (test hook; no GPU needed). */
+void fmx_debug_exact_fold(const double* x, int64_t n, int64_t* limbs_out, double* value_out);
 /* The builder-defined corr_prune selector for J rolling windows in one call:
  * per-date Gram partials of the raw panel X (z-scored with stats [F][D][2] from
  * fmx_cs_moment_stats) for every date any window touches, then per window j the pooled

@@ -66,6 +66,17 @@ class OracleBackend:
         Z, M = OG.zscore_exposures(X.numpy())
         return torch.from_numpy(Z), torch.from_numpy(M)
 
+    def corr_gram_exact(self, X, d0, d1, stats=None, z=None):
+        """Exact fixed-point Gram partials of dates [d0, d1) (one fold unit per date)."""
+        Z, M = OG.zscore_exposures(X[:, d0:d1].numpy())
+        limbs, counts = OG.gram_exact_parts(Z, M)
+        return torch.from_numpy(limbs), torch.from_numpy(counts)
+
+    @staticmethod
+    def gram_exact_finalize(limbs, counts):
+        G, N = OG.gram_exact_finalize(limbs.numpy(), counts.numpy())
+        return torch.from_numpy(G), torch.from_numpy(N)
+
     def gram(self, Z, M):
         Zf = Z.reshape(Z.shape[0], -1).double()
         Mf = M.reshape(M.shape[0], -1).double()

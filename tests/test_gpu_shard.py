@@ -1,0 +1,113 @@
+"""C3 on the HIP path: the date-sharded step (BASELINE configs[2]) with the
+product EngineBackend, its N shards run as N in-process threads on one MI355X
+(factormodeling_amd.comm.LocalComm: halo send/recv, IC all-gather and the exact Gram
+all-reduce are device copies ordered by HIP events), compared with the 1-shard HIP run of
+the same panel; plus the exact Gram's split invariance on the device.
+
+Tolerances: cross-sectional outputs, the daily IC series, window metrics, selections, the
+correlation matrix C and the kept set are bit-identical at every shard count (C by the
+exact fixed-point Gram, fmx_gram_exact); rolling outputs on owned dates restart their
+Kahan/Welford state at the halo, so they agree to <= 1e-12 relative."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _one_shard(dev, D, A, F, cfg, seed):
+    import torch
+    from factormodeling_amd import pipeline as PL
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=seed, halo=cfg.halo)
+    col = {}
+    w, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    return w.cpu().numpy(), kept, {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in col.items()}
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_step_hip_matches_one_shard(dev, world):
+    import torch
+    from factormodeling_amd import pipeline as PL
+    from factormodeling_amd.comm import run_local_shards
+    D, A, F = 200, 700, 12
+    cfg = PL.StepConfig(sel_window=60)
+    w1, kept1, col1 = _one_shard(dev, D, A, F, cfg, 11)
+
+    def shard(rank, comm):
+        sp = PL.ShardedPanel(D, A, F, device=dev, seed=11, halo=cfg.halo, comm=comm)
+        assert sp.halo == (cfg.halo if rank else 0)
+        col = {}
+        w, kept = PL.run_step(sp, cfg, collect=col)
+        torch.cuda.current_stream().synchronize()
+        return (sp.d_lo, sp.d_hi, w.cpu().numpy(), kept,
+                {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in col.items()})
+
+    res = run_local_shards(world, shard)
+    assert [r[0] for r in res] == [PL.shard_bounds(D, world, r)[0] for r in range(world)]
+    for lo, hi, w, kept, col in res:
+        assert np.array_equal(w, w1), lo                              # selections
+        assert kept == kept1, lo                                     # pruned set
+        assert np.array_equal(col["C"], col1["C"]), lo               # exact Gram: same bits
+        assert np.array_equal(col["daily"], col1["daily"], equal_nan=True), lo   # gathered IC series
+        for k in ("summ", "win"):
+            assert np.array_equal(col[k], col1[k], equal_nan=True), (lo, k)
+        for kind, op, wn in cfg.ops:
+            k = f"{kind}:{op or ''}:{wn or ''}"
+            got, ref = col[k], col1[k][:, lo:hi]
+            if kind == "ts":
+                np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-13, equal_nan=True, err_msg=k)
+            else:
+                assert np.array_equal(got, ref, equal_nan=True), (lo, k)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("F,A", [(12, 700), (200, 777), (37, 5000)])
+def test_gram_exact_split_invariant_on_device(dev, F, A):
+    """fmx_gram_exact over any split of the dates, limbs summed as integers, finalizes to
+    the same G / N bits as one launch; and agrees with the oracle's Gram."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F + A)
+    D = 23
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.03] = np.nan
+    X[0, 4] = 1.5                                   # constant row: sigma 0 -> invalid
+    Xd = torch.as_tensor(X, device=dev)
+    _, stats = E.cs_moment_stats("stats", Xd)
+    L1, N1 = E.gram_exact(Xd, stats, 0, D)
+    G1, Nf1 = E.gram_exact_finalize(L1, N1)
+    for cuts in ([11], [1, 2, 17], [5, 6, 7, 8, 9, 22]):
+        b = [0] + cuts + [D]
+        L = torch.zeros_like(L1)
+        N = torch.zeros_like(N1)
+        for a0, a1 in zip(b[:-1], b[1:]):
+            la, na = E.gram_exact(Xd, stats, a0, a1)
+            L += la
+            N += na
+        G, Nf = E.gram_exact_finalize(L, N)
+        assert torch.equal(G, G1) and torch.equal(Nf, Nf1), cuts
+    Z, M = OG.zscore_exposures(X)
+    Zf, Mf = Z.reshape(F, -1), M.reshape(F, -1)
+    np.testing.assert_allclose(G1.cpu().numpy(), Zf @ Zf.T, rtol=1e-11, atol=1e-9)
+    assert np.array_equal(Nf1.cpu().numpy(), Mf @ Mf.T)
+    # accumulate=True adds into existing limbs
+    L2, N2 = E.gram_exact(Xd, stats, 0, 11)
+    E.gram_exact(Xd, stats, 11, D, limbs=L2, counts=N2, accumulate=True)
+    G2, _ = E.gram_exact_finalize(L2, N2)
+    assert torch.equal(G2, G1)
+    # the z-score input path gives the same partials as the stats path (same z arithmetic)
+    Zd = E.cs_moment("zscore", Xd)
+    Lz, Nz = E.gram_exact(Zd, None, 0, D)
+    Gz, Nzf = E.gram_exact_finalize(Lz, Nz)
+    np.testing.assert_allclose(Gz.cpu().numpy(), G1.cpu().numpy(), rtol=1e-12, atol=1e-9)
+    assert torch.equal(Nzf, Nf1)

@@ -1,4 +1,4 @@
-"""Date-sharded multi-rank step on CPU (gloo, world_size 2) vs a single-rank run.
+"""Date-sharded multi-rank step on CPU (gloo, world_size 2 and 3) vs a single-rank run.
 
 The product's distributed logic (factormodeling_amd.pipeline: halo exchange by
 send/recv, IC all-gather, Gram all-reduce, redundant selection) runs unchanged; the
@@ -82,7 +82,8 @@ def test_sharded_step_matches_single_rank(world):
     for rank, lo, hi, w, kept, C, summ, ops in res:
         assert np.array_equal(w, w1.numpy()), rank            # selections identical on every rank
         assert kept == kept1, rank
-        np.testing.assert_allclose(C, col["C"].numpy(), rtol=1e-12, atol=1e-14)
+        # the Gram is an exact integer fixed-point sum: the same bits at every rank count
+        assert np.array_equal(C, col["C"].numpy()), rank
         np.testing.assert_allclose(summ, col["summ"].numpy(), rtol=1e-12, atol=1e-14, equal_nan=True)
         for k, v in ops.items():                               # operators on owned dates (halo warm-up)
             ref = col[k].numpy()[:, lo:hi]
@@ -113,3 +114,40 @@ def test_shard_bounds_cover_dates():
         assert spans[0][0] == 0 and spans[-1][1] == 2520
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
     assert PL.HALO >= max(w for k, o, w in PL.OPS if w) - 1 + 2
+
+
+def test_rank_owning_fewer_dates_than_halo_is_rejected():
+    """a sending rank with fewer owned dates than the halo would ship its own
+    not-yet-received halo rows; the sharding is rejected up front."""
+    from factormodeling_amd import pipeline as PL
+    with pytest.raises(ValueError, match="owns"):
+        PL.check_sharding(50, 3, 21)        # 17 dates per rank < halo 21
+    with pytest.raises(ValueError, match="owns"):
+        PL.check_sharding(5, 8, 1)          # ranks with no dates at all
+    PL.check_sharding(90, 3, 21)
+    PL.check_sharding(2520, 8, 61)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_comm_shards_match_gloo_semantics(world):
+    """The in-process LocalComm (threads; the GPU test's transport) gives the same results
+    as the 1-rank step, bit for bit on C and the selections (oracle backend, CPU)."""
+    from factormodeling_amd import pipeline as PL
+    from factormodeling_amd.comm import run_local_shards
+    cfg = PL.StepConfig(sel_window=W)
+
+    def shard(rank, comm):
+        sp = PL.ShardedPanel(D, A, F, device=torch.device("cpu"), seed=3, comm=comm)
+        col = {}
+        w, kept = PL.run_step(sp, cfg, be=OracleBackend(), collect=col)
+        return sp.d_lo, sp.d_hi, w.numpy(), kept, col["C"].numpy(), {k: v.numpy() for k, v in col.items() if ":" in k}
+
+    res = run_local_shards(world, shard)
+    sp = PL.ShardedPanel(D, A, F, 0, 1, torch.device("cpu"), seed=3)
+    col = {}
+    w1, kept1 = PL.run_step(sp, cfg, be=OracleBackend(), collect=col)
+    for lo, hi, w, kept, C, ops in res:
+        assert np.array_equal(w, w1.numpy()) and kept == kept1
+        assert np.array_equal(C, col["C"].numpy())
+        for k, v in ops.items():
+            np.testing.assert_allclose(v, col[k].numpy()[:, lo:hi], rtol=1e-12, atol=1e-12, equal_nan=True, err_msg=k)
