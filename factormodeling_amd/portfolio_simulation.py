@@ -13,13 +13,19 @@ the GPU through libfmx:
   (``k_pnl_contrib``);
 * ``_calculate_metrics`` (:799-819): the daily IC (``k_daily_corr``).
 
-The MVO methods solve a cvxpy / scipy QP per date on the host; they are not part of the
-device path and raise ``NotImplementedError`` here.  ``PortfolioAnalyzer`` (reporting and
-plots) is the reference's own host module, imported from ``portfolio_analyzer`` when
-``run()`` needs it.
+The MVO methods ('mvo', 'mvo_turnover', :183-248, :315-746) solve a cvxpy / scipy QP per
+date on the host and stay the reference's own code: ``_daily_trade_list`` hands them to the
+reference's ``Simulation``, loaded by file path from ``FMX_REFERENCE_DIR`` (the user's
+reference checkout; a module of the same name cannot sit on ``sys.path`` next to this
+drop-in), while the P&L and metrics of the resulting weights still run on the device.
+``PortfolioAnalyzer`` (reporting and plots) is the reference's own host module, imported
+from ``portfolio_analyzer`` when ``run()`` needs it.
 """
 from __future__ import annotations
 
+import importlib.util
+import os
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -57,6 +63,31 @@ class SimulationSettings:
     shrinkage_intensity: float = 0.1
     turnover_penalty: float = 0.1
     return_weight: float = 0.0
+
+
+_REF_MODULE = None
+
+
+def reference_simulation_classes():
+    """(Simulation, SimulationSettings) of the reference's ``portfolio_simulation.py``,
+    loaded by path from ``$FMX_REFERENCE_DIR`` under a private module name (cached).  Its
+    own imports (``portfolio_analyzer``, cvxpy, scipy) resolve as in the reference checkout;
+    the directory is appended to ``sys.path`` for ``portfolio_analyzer`` if needed."""
+    global _REF_MODULE
+    if _REF_MODULE is None:
+        d = os.environ.get("FMX_REFERENCE_DIR")
+        path = os.path.join(d, "portfolio_simulation.py") if d else None
+        if not path or not os.path.exists(path):
+            raise NotImplementedError(
+                "methods 'mvo' / 'mvo_turnover' run the reference's host QP solvers: set FMX_REFERENCE_DIR to the "
+                "FactorModeling checkout that holds portfolio_simulation.py")
+        if d not in sys.path:
+            sys.path.append(d)
+        spec = importlib.util.spec_from_file_location("_fmx_reference_portfolio_simulation", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _REF_MODULE = mod
+    return _REF_MODULE.Simulation, _REF_MODULE.SimulationSettings
 
 
 class _Grid:
@@ -141,12 +172,24 @@ class Simulation:
     # ----------------------------------------------------------------------------- trade list
     def _daily_trade_list(self):
         """portfolio_simulation.py:96-154 (equal / linear on the device)."""
+        if self.method in ("mvo", "mvo_turnover"):
+            return self._host_trade_list()
         if self.method not in ("equal", "linear"):
-            if self.method in ("mvo", "mvo_turnover"):
-                raise NotImplementedError(f"method {self.method!r} solves a cvxpy QP per date on the host; "
-                                          "the device path runs 'equal' and 'linear'")
             raise ValueError(f"Unknown method {self.method}")
         return daily_trade_list(self.custom_feature, self.pct, self.method, self.max_weight)
+
+    def _host_trade_list(self):
+        """'mvo' / 'mvo_turnover': the reference's own per-date QP loop
+        (portfolio_simulation.py:96-154 with :183-248, :315-746), run on a reference
+        ``Simulation`` that carries this instance's state (the investability-masked signal,
+        settings and any attribute changed since construction)."""
+        cls, settings_cls = reference_simulation_classes()
+        from dataclasses import fields
+        ref_settings = settings_cls(**{f.name: getattr(self.settings, f.name) for f in fields(settings_cls)})
+        ref = cls(self.name, self.custom_feature, ref_settings)
+        ref.__dict__.update(self.__dict__)
+        ref.settings = ref_settings
+        return ref._daily_trade_list()
 
     @staticmethod
     def _normalize_legs(weights: pd.Series) -> pd.Series:
