@@ -241,9 +241,13 @@ def group_op(op: str, X, G, ngroups: int, method="average", present=None):
     if G.dtype != torch.int32 or tuple(G.shape) != (D, A):
         raise _lib.FmxError("G must be int32 [D][A]")
     if op == "rank" and A > 4096 and ngroups > 0:
-        ok = G >= 0 if present is None else (G >= 0) & (present != 0)
+        # codes outside [0, ngroups) belong to no group (the kernel sorts them past the last
+        # boundary); clamp the index so the count never writes out of bounds
+        ok = (G >= 0) & (G < ngroups)
+        if present is not None:
+            ok &= present != 0
         cnt = torch.zeros((D, ngroups), dtype=torch.int32, device=G.device)
-        cnt.scatter_add_(1, G.clamp_min(0).long(), ok.int())
+        cnt.scatter_add_(1, G.clamp(0, ngroups - 1).long(), ok.int())
         if int(cnt.max()) > 8192:
             raise _lib.FmxError("group_rank_normalized on rows > 4096 assets sorts each group in LDS: "
                                 "at most 8192 members per (date, group)")

@@ -116,6 +116,12 @@ class _Grid:
             m[self.dates.get_indexer(s.index.get_level_values(0).unique())] = True
         return m
 
+    def symbol_mask(self, s):
+        m = np.zeros(self.A, dtype=bool)
+        if s is not None and len(s):
+            m[self.symbols.get_indexer(pd.Index(np.asarray(s.index.get_level_values(1).unique(), dtype=object)))] = True
+        return m
+
 
 class Simulation:
     """Runs a daily long/short simulation given a factor series and SimulationSettings
@@ -244,6 +250,11 @@ class Simulation:
         ], axis=1).reset_index().sort_values("date", ascending=False).reset_index(drop=True)
         if self.contributor:
             cb = contrib.cpu().numpy()
+            # the reference subtracts two Series indexed by weights ∪ returns and weights ∪
+            # cap_flag symbols (:793-794): a symbol outside either set aligns to NaN, which
+            # nlargest drops
+            ws, rs, cs = (g.symbol_mask(s) for s in (weights, self.returns, self.cap_flag))
+            cb = np.where(((ws | rs) & (ws | cs))[:, None], cb, np.nan)
             longs_pnl = pd.Series(cb[:, 0], index=g.symbols)
             shorts_pnl = pd.Series(cb[:, 1], index=g.symbols)
             return result, longs_pnl.nlargest(10), shorts_pnl.nlargest(10)
