@@ -52,6 +52,10 @@ def bytes_per_unit(stage, F, ranked=False):
         return 24.0
     if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u16)
         return 26.0 if ranked else 24.0
+    if kind == "cs_rank_winsor_ic":     # X once + two outputs + two R rows per (f, date); no ranks
+        return 24.0 + 16.0 / F
+    if kind == "rank_ic":               # ranks-only pass with the IC fused: X once + two R rows
+        return 8.0 + 16.0 / F
     if kind == "rank2":              # ranks-only pass: X once + the u16 doubled ranks
         return 10.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
@@ -64,7 +68,8 @@ def bytes_per_unit(stage, F, ranked=False):
 # stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
                 "ts_set": "fmx::k_ts_set<", "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
-                "cs_rank_winsor": "fmx::k_cs_rank_fa<",
+                "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
+                "rank_ic": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",
                 "cs:market_neutralize": "fmx::k_cs_moment<2>", "ts:mean": "fmx::k_ts_reg<1,",

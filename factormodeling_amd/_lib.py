@@ -44,6 +44,9 @@ SIGNATURES = {
     "fmx_ic_daily": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
     "fmx_ic_ranked_work_len": [c_i64, c_i64],
     "fmx_ic_daily_ranked": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp],
+    "fmx_rank_ic_work_len": [c_i64, c_i64, c_i64],
+    "fmx_cs_rank_winsor_ic": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_i32, c_vp, c_vp,
+                              c_i64, c_vp, c_vp],
     "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
     "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
@@ -75,7 +78,7 @@ SIGNATURES = {
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
+_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
              "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
              "fmx_debug_exact_fold": None}

@@ -335,6 +335,24 @@ extern "C" fmx_status fmx_ic_daily_ranked(const double* X, const fmx_rank2_t* ra
   return br_ic_ranked(X, rank2, R, F, D, A, ld, lags, n_lags, out, work, as_stream(stream));
 }
 
+extern "C" int64_t fmx_rank_ic_work_len(int64_t F, int64_t D, int64_t A) { return rank_ic_work_len(F, D, A); }
+
+extern "C" fmx_status fmx_cs_rank_winsor_ic(const double* X, double* Yrank, double* Ywinsor, const double* R,
+                                            int64_t F, int64_t D, int64_t A, int64_t ld, double qlo, double qhi,
+                                            const int32_t* lags, int32_t n_lags, fmx_rank2_t* rank2, int32_t* work,
+                                            int64_t work_len, double* out, void* stream) {
+  FMX_ARG(X && R && out && lags && rank2 && work, "null pointer");
+  FMX_ARG((Yrank == nullptr) == (Ywinsor == nullptr), "Yrank and Ywinsor: both or neither");
+  FMX_ARG(!Yrank || (Yrank != X && Ywinsor != X && Yrank != Ywinsor), "outputs must be distinct from X and each other");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
+  FMX_ARG(n_lags >= 1 && n_lags <= 2, "n_lags 1 or 2");
+  FMX_ARG(work_len >= rank_ic_work_len(F, D, A), "work shorter than fmx_rank_ic_work_len(F, D, A)");
+  for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  return br_cs_rank_winsor_ic(X, Yrank, Ywinsor, R, F, D, A, ld, qlo, qhi, lags, n_lags, rank2, work, out,
+                              as_stream(stream));
+}
+
 extern "C" fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev,
                                     const int32_t* d1_dev, int64_t J, double* out, void* stream) {
   FMX_ARG(daily && d0_dev && d1_dev && out, "null pointer");

@@ -27,8 +27,9 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   double* Y2 = nullptr;
   double qlo = 0.0, qhi = 0.0;
   fmx_rank2_t* RK = nullptr;
+  FrIc ic{};
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
@@ -49,8 +50,9 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   int method = FMX_RANK_AVERAGE;
+  FrIc ic{};
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK};
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;
@@ -71,8 +73,9 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   int method = FMX_RANK_AVERAGE;
   const uint8_t* present = nullptr;
   double qlo = 0.0, qhi = 0.0;
+  FrIc ic{};
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;

@@ -40,6 +40,275 @@ constexpr int FR_K_CS = 247;   // fine buckets per interval (cs_rank: 16-bit cou
 constexpr int FR_CS_WORDS = 8192;
 constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows fit a CU)
 
+// Daily IC fused into the rank pass (k_cs_rank_fa<..., IC = true>): the workgroup that
+// ranks row (f, s) also reduces the pairs (X[f][s], R[s + L_m]) of up to two lags, so the
+// ranks never leave the CU (factor_selector.py:36-48).  Rows run date-major (workgroup b
+// -> s = b / F, f = b % F): the F rows of a date share its return rows in L2.
+struct FrIc {
+  const double* Rt;          // returns [D][ld]
+  const uint32_t* nanb;      // NaN-return bits [D][nw] (k_ret_rows)
+  const double* rsh;         // [D] first non-NaN return of each date (0 if none): moment anchor
+  int64_t F, nw;
+  int L0, L1, NL;
+  double* out;               // [NL][4][F][D] = (n, IC, rank IC, beta) at target date s + L
+  int32_t* ovf;              // [1 + F*D]: rows whose NaN-return list exceeds FR_IC_EC
+  fmx_rank2_t* RK;           // the doubled ranks of those rows (k_ic_ranked_list input)
+};
+constexpr int FR_IC_EC = 256;  // E entries per lag held in LDS; longer lists: ovf
+#ifndef FR_IC_CH
+#define FR_IC_CH 2             // return loads in flight per thread in the IC pass
+#endif
+
+struct FrIcRow {
+  int64_t s, f;              // source date, factor
+  int lag[2];
+  bool act[2];               // lag m has a target date s + L_m < D
+};
+
+__device__ __forceinline__ FrIcRow fr_ic_row(const FrIc& ic, int64_t D) {
+  FrIcRow r;
+  r.s = (int64_t)blockIdx.x / ic.F;
+  r.f = (int64_t)blockIdx.x % ic.F;
+  r.lag[0] = ic.L0;
+  r.lag[1] = ic.L1;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) r.act[m] = m < ic.NL && r.s + r.lag[m] < D;
+  return r;
+}
+
+__device__ __forceinline__ void fr_ic_put(const FrIc& ic, int64_t D, const FrIcRow& rw, int m, double nn, double icv,
+                                          double ric, double beta) {
+  double* o = ic.out + ((int64_t)(m * 4) * ic.F + rw.f) * D + rw.s + rw.lag[m];
+  const int64_t stp = ic.F * D;
+  o[0] = nn;
+  o[stp] = icv;
+  o[2 * stp] = ric;
+  o[3 * stp] = beta;
+}
+
+// IC tail of k_cs_rank_fa<..., IC>: every thread calls it once the row's ranks are known,
+// a barrier has retired every read of the bucketed keys and the row's exposures sit in LDS
+// (xk[i]: the key registers are free again).  lds: the scratch after xk.  r2: the thread's
+// doubled ranks among the row's non-NaN exposures (0: NaN), two per word; em: bit 2k+m set when element k is non-NaN and its lag-m return is NaN.  The
+// pairs of lag m are the non-NaN exposures minus that list E_m; a pair's rank is r2 minus
+// #(E_m < x) + #(E_m <= x), read off a 64-rank block table of E_m (as k_ic_wave).
+// Moments: one pass of sums shifted by block-uniform anchors (xs: a sample key of the
+// row, ic.rsh[t]: the target date's first non-NaN return), so wave partials simply add
+// (records agree with the two-pass kernels to ~1e-15 relative, pair counts exactly).
+// dynamic LDS of the IC variant: the row's exposures (A doubles), then the tail's E lists,
+// block tables and wave partials
+__host__ __device__ inline int64_t fr_ic_xk_words(int64_t A) { return (A * 8 + 15) / 16 * 4; }
+__host__ __device__ inline int64_t fr_ic_lds_bytes(int64_t A, int nt) {
+  const int64_t nbp = (((2 * A) >> 6) + 2) & ~1ll;
+  return fr_ic_xk_words(A) * 4 + (2 * FR_IC_EC + 2 * nbp) * 4 + (int64_t)(nt / 64 + 1) * 20 * 8;
+}
+
+template <int EMAX>
+__device__ __forceinline__ uint32_t fr_r2(const uint32_t* r2, int k) {
+  return (r2[k / 2] >> (16 * (k % 2))) & 0xffffu;
+}
+
+template <int NT, int EMAX>
+__device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, int64_t D, int64_t A, int64_t ld,
+                                           int64_t row, const double* xk, const uint32_t* r2, uint32_t em,
+                                           bool last_in, double xs, uint32_t* lds, int* ne BR_PH_PARAMS) {
+  constexpr int NW = NT / 64, S = 20;        // per-wave scratch: 2 lags x 8 sums, 2 x (count, flags)
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int nb = (int)((2 * A) >> 6) + 1;     // doubled ranks are <= 2A
+  const int nbp = (nb + 1) & ~1;
+  uint32_t* ebuf = lds;                       // [2][FR_IC_EC] E entries (unordered, then by block)
+  uint32_t* T = lds + 2 * FR_IC_EC;           // [2][nbp] block table: start | end << 16
+  double* scr = reinterpret_cast<double*>(lds + 2 * FR_IC_EC + 2 * nbp);
+  // 1. unordered E lists
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if ((em >> (2 * k + m)) & 1) {
+        const int q = atomicAdd(&ne[m], 1);
+        if (q < FR_IC_EC) ebuf[m * FR_IC_EC + q] = fr_r2<EMAX>(r2, k);
+      }
+    }
+  }
+  // lag 0's returns in flight over the table build
+  const bool last_ok = last_in;
+  auto pair_of = [&](int k, int m) {           // non-NaN exposure (r2 > 0), non-NaN return
+    return (k < EMAX - 1 || last_ok) && fr_r2<EMAX>(r2, k) != 0u && !((em >> (2 * k + m)) & 1);
+  };
+  // unconditional loads (a branch per load serialises them): the last slot clamped into
+  // the row, inactive lags read date s's row; non-pairs are skipped when summing
+  const int ilast = (EMAX - 1) * NT + t < (int)A ? (EMAX - 1) * NT + t : (int)A - 1;
+  auto load_r = [&](double* rv, const double* rr) {
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) rv[k] = rr[k < EMAX - 1 ? t + k * NT : ilast];
+  };
+  double rv[EMAX];
+  load_r(rv, ic.Rt + (rw.act[0] ? rw.s + rw.lag[0] : rw.s) * ld);
+  BR_PH();
+  __syncthreads();
+  BR_PH();
+  const int nE[2] = {ne[0], ne[1]};
+  if ((rw.act[0] && nE[0] > FR_IC_EC) || (rw.act[1] && nE[1] > FR_IC_EC)) {
+    // a long NaN-return list: k_ic_ranked_list takes the row from its doubled ranks
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (k < EMAX - 1 || last_in) ic.RK[row * ld + t + k * NT] = (fmx_rank2_t)fr_r2<EMAX>(r2, k);
+    if (t == 0) {
+      const int q = atomicAdd(&ic.ovf[0], 1);
+      ic.ovf[1 + q] = (int32_t)blockIdx.x;
+    }
+    return;
+  }
+  // 2. wave m counting-sorts lag m's entries into 64-rank blocks
+  const bool wact = wid == 0 ? rw.act[0] : rw.act[1];   // (no dynamic register-array index)
+  const int c = wid == 0 ? nE[0] : nE[1];
+  if (wid < 2 && wact && c > 0) {
+    uint32_t* Tm = T + wid * nbp;
+    uint32_t* eb = ebuf + wid * FR_IC_EC;
+    for (int b = lane; b < nbp; b += 64) Tm[b] = 0u;
+    uint32_t er[FR_IC_EC / 64];
+    int es[FR_IC_EC / 64];
+#pragma unroll
+    for (int q = 0; q < FR_IC_EC / 64; ++q) {
+      const int j = 64 * q + lane;
+      er[q] = j < c ? eb[j] : 0u;             // entries are doubled ranks >= 2
+      es[q] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < FR_IC_EC / 64; ++q)
+      if (er[q]) es[q] = (int)atomicAdd(&Tm[er[q] >> 6], 1u);
+    __builtin_amdgcn_wave_barrier();
+    const int R = (nbp + 63) >> 6;            // lane l owns blocks [l R, l R + R)
+    int loc = 0;
+    for (int q = 0; q < R; ++q) {
+      const int b = lane * R + q;
+      loc += b < nbp ? (int)Tm[b] : 0;
+    }
+    int incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = fr_up(incl, o, lane);
+      if (lane >= o) incl += u;
+    }
+    int run = incl - loc;
+    for (int q = 0; q < R; ++q) {
+      const int b = lane * R + q;
+      if (b < nbp) {
+        const int n = (int)Tm[b];
+        Tm[b] = (uint32_t)run | ((uint32_t)(run + n) << 16);
+        run += n;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < FR_IC_EC / 64; ++q)
+      if (er[q]) eb[(Tm[er[q] >> 6] & 0xffffu) + es[q]] = er[q];
+  }
+  BR_PH();
+  __syncthreads();
+  BR_PH();
+  // 3. per lag: pair count (ballots), sums about the anchors (xs, ar), exact integer rank
+  // sums; wave partials into scr
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int cnt = 0;
+    uint32_t dif = 0;
+    if (rw.act[m]) {                          // block-uniform
+      const double* rr = ic.Rt + (rw.s + rw.lag[m]) * ld;
+      if (m == 1) load_r(rv, rr);
+      const double ar = ic.rsh[rw.s + rw.lag[m]];
+      const uint32_t* Tm = T + m * nbp;
+      const uint32_t* eb = ebuf + m * FR_IC_EC;
+      const bool hasE = nE[m] > 0;
+      uint64_t kk = 0;
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        const bool pair = pair_of(k, m);
+        cnt += __popcll(__ballot(pair));
+        if (!pair) continue;
+        const double x = xk[t + k * NT], r = rv[k];
+        uint32_t k2 = fr_r2<EMAX>(r2, k);
+        if (hasE) {
+          const uint32_t tb = Tm[k2 >> 6];
+          const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16;
+          uint32_t corr = 2u * j0;
+          for (uint32_t j = j0; j < j1; ++j) {  // this block's entries (usually none)
+            const uint32_t e = eb[j];
+            corr += (e < k2 ? 1u : 0u) + (e <= k2 ? 1u : 0u);
+          }
+          k2 -= corr;
+        }
+        const double dx = x - xs, dy = r - ar;
+        dif |= ((x != xs) ? 1u : 0u) | ((r != ar) ? 2u : 0u);
+        a[0] += dx; a[1] += dy;
+        a[2] += dx * dx; a[3] += dy * dy; a[4] += dx * dy;
+        a[5] += (double)k2 * dy;
+        kk += (uint64_t)k2 * k2;
+      }
+      a[7] = (double)kk;                      // a[6] unused (sum k = n(n+1) exactly)
+    }
+    fr_part_bfly<8, false>(a, scr, S, 8 * m);
+    const uint32_t fl = (__ballot(dif & 1u) != 0 ? 1u : 0u) | (__ballot(dif & 2u) != 0 ? 2u : 0u);
+    if (lane == 0) {
+      scr[wid * S + 16 + 2 * m] = (double)cnt;
+      scr[wid * S + 17 + 2 * m] = (double)fl;
+    }
+    BR_PH();
+  }
+  __syncthreads();
+  BR_PH();
+  // 4. wave 0: lane j < 20 totals value j over the waves (counts and sums add, flags OR);
+  // lane 0 finishes both lags' records
+  if (wid == 0) {
+    double v = 0.0;
+    uint32_t orf = 0;
+    if (lane < S) {
+      for (int w = 0; w < NW; ++w) {
+        const double x = scr[w * S + lane];
+        v += x;
+        if (lane == 17 || lane == 19) orf |= (uint32_t)x;
+      }
+    }
+    // totals through LDS (20 readlanes would hold 40 SGPRs and spill)
+    double* tot = scr + NW * S;
+    if (lane < S) tot[lane] = (lane == 17 || lane == 19) ? (double)orf : v;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+      const uint32_t fl0 = (uint32_t)tot[17], fl1 = (uint32_t)tot[19];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        if (!rw.act[m]) continue;
+        const double* w = tot + 8 * m;
+        const double n = tot[16 + 2 * m];
+        const uint32_t fl = m == 0 ? fl0 : fl1;
+        double icv = qnan(), ric = qnan(), beta = qnan();
+        if (n >= 3.0) {
+          const double s1 = w[0], s2 = w[1];
+          if ((fl & 3u) == 3u) {              // neither side constant
+            const double cxy = w[4] - s1 * s2 / n;
+            const double cxx = w[2] - s1 * s1 / n;
+            const double cyy = w[3] - s2 * s2 / n;
+            // ranks: sum k = n(n+1)/2 (ties keep it), sum k^2 = sum (2k)^2 / 4: both exact
+            const double ckk = w[7] / 4.0 - n * (n + 1.0) * (n + 1.0) / 4.0;
+            const double cky = 0.5 * w[5] - 0.5 * (n + 1.0) * s2;
+            icv = fmin(1.0, fmax(-1.0, cxy / sqrt(cxx * cyy)));
+            ric = fmin(1.0, fmax(-1.0, cky / sqrt(ckk * cyy)));
+          }
+          // beta = sum x r / sum x^2 from the shifted sums
+          const double a = xs, b = ic.rsh[rw.s + rw.lag[m]];
+          const double sxx_raw = w[2] + 2.0 * a * s1 + n * a * a;
+          const double sxr_raw = w[4] + a * s2 + b * s1 + n * a * b;
+          beta = sxx_raw > 0 ? sxr_raw / sxx_raw : qnan();
+        }
+        fr_ic_put(ic, D, rw, m, n, icv, ric, beta);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // cs_rank: y = (rank - 1) / (len(row) - 1), len counting NaN rows; 0.5 for single-row
 // dates (operations.py:58-60).  Rows are (f, d) = blockIdx.x / D, % D.
@@ -58,11 +327,14 @@ constexpr int FR_K_IC = 62;    // (IC: 64-bit packed counters, 32 KB: two rows f
 // RK (optional): 2 * average rank among the row's valid keys, i.e. 2*#less + #equal + 1
 // (0 for NaN / absent), as uint16 (<= 2A) -- the daily IC of the same rows starts from it
 // (k_ic_wave) instead of ranking them again.
-template <int NT, int EMAX, bool PRES, bool WQ = false>
+//
+// IC (dense rows, method average): the daily IC records of the row's two lags from its
+// ranks (fr_ic_tail) -- no doubled ranks written, no second pass over X.
+template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false>
 __global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
-             fmx_rank2_t* __restrict__ RK) {
+             fmx_rank2_t* __restrict__ RK, FrIc ic) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
@@ -74,7 +346,14 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   uint64_t* bkey = lds;
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
-  const int64_t row = blockIdx.x;
+  static_assert(!(IC && PRES), "the fused IC ranks dense rows");
+  FrIcRow rw{};
+  __shared__ int ic_ne[2];                    // E-list lengths (IC)
+  if constexpr (IC) {
+    rw = fr_ic_row(ic, D);
+    if (t < 2) ic_ne[t] = 0;
+  }
+  const int64_t row = IC ? rw.f * D + rw.s : (int64_t)blockIdx.x;
   const double* x = X + row * ld;
   double* y = Y + row * ld;
   const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
@@ -83,11 +362,23 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   uint64_t key[EMAX];
   uint32_t pm = 0, hmin = 0xffffffffu, hmax = 0u;
   int wv = 0, wp = 0;                         // wave-uniform counts (ballots)
+  // every load of the row issued before the first is consumed: a load under a branch (the
+  // key conversion below is one per element) waits out the previous one's HBM latency.
+  // The last slot is clamped into the row (its value is unused when out of range).
+  const int ilast = last_in ? t + (EMAX - 1) * NT : (An > 0 ? An - 1 : 0);
+  double xv[EMAX];
+  uint32_t pv = 0;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? t + k * NT : ilast];
+  if (PRES) {
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) pv |= (prow[k < EMAX - 1 ? t + k * NT : ilast] != 0 ? 1u : 0u) << k;
+  }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     const bool in = k < EMAX - 1 || last_in;
-    const double v = in ? x[t + k * NT] : 0.0;
-    const bool p = in && (PRES ? prow[t + k * NT] != 0 : true);
+    const double v = xv[k];
+    const bool p = in && (PRES ? ((pv >> k) & 1u) != 0 : true);
     const bool ok = p && v == v;
     pm |= (uint32_t)p << k;
     key[k] = ok ? okey(v) : KEY_SENTINEL;
@@ -135,6 +426,17 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
         if (k < EMAX - 1 || last_in) Y2[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+    }
+    if constexpr (IC) {                       // < 3 pairs: empty records (n = 0, or 1 on a one-asset row)
+      if (t == 0) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          if (!rw.act[m]) continue;
+          const double r = ic.Rt[(rw.s + rw.lag[m]) * ld];
+          const double n = (nv > 0 && key[0] != KEY_SENTINEL && r == r) ? 1.0 : 0.0;
+          fr_ic_put(ic, D, rw, m, n, qnan(), qnan(), qnan());
+        }
+      }
     }
     return;
   }
@@ -212,11 +514,15 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       }
     }
   }
+  uint32_t r2[IC ? (EMAX + 1) / 2 : 1];       // IC: doubled ranks (0: NaN), two 16-bit per word
+  uint32_t em = 0;                            // IC: bit 2k+m = non-NaN exposure, NaN lag-m return
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
+    if constexpr (IC) if (k % 2 == 0) r2[k / 2] = 0u;
     if (!(k < EMAX - 1 || last_in)) continue;
     const int lt = le[k] & 0xffff, eq = le[k] >> 16;
     const int less = (sl[k] & 0xffff) + lt;
+    if constexpr (IC) r2[k / 2] |= (key[k] != KEY_SENTINEL ? (uint32_t)(2 * less + eq + 1) : 0u) << (16 * (k % 2));
     double r;
     if (method == FMX_RANK_MIN) r = (double)(less + 1);
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
@@ -229,6 +535,20 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (less <= kk[j] && kk[j] < less + eq) tval[j] = key[k];   // all writers store the same key
+    }
+  }
+  if constexpr (IC) {
+    // E membership: non-NaN exposure whose lag-m return is NaN (bit rows of k_nan_bits)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if (!rw.act[m]) continue;
+      const uint32_t* nb = ic.nanb + (rw.s + rw.lag[m]) * ic.nw;
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) {
+        const int i = (k < EMAX - 1 || last_in) ? t + k * NT : 0;   // unconditional loads
+        const uint32_t bit = (nb[i >> 5] >> (i & 31)) & 1u;
+        if ((k < EMAX - 1 || last_in) && key[k] != KEY_SENTINEL) em |= bit << (2 * k + m);
+      }
     }
   }
   if (WQ) {
@@ -255,6 +575,20 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
       __builtin_nontemporal_store((PRES && !((pm >> k) & 1)) ? qnan() : o, y2 + t + k * NT);
     }
+  }
+  if constexpr (IC) {
+    if constexpr (!WQ) __syncthreads();       // (WQ: its barrier) every in-bucket scan read is done
+    // the exposures move to LDS (read once per lag by their owner): frees the key registers
+    double* xk = reinterpret_cast<double*>(lds);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (k < EMAX - 1 || last_in) xk[t + k * NT] = key[k] != KEY_SENTINEL ? okey_inv(key[k]) : 0.0;
+    // exposure anchor: a sample key of the row (block-uniform, the sorted samples in tab)
+    const uint64_t sk = tab.spl[31] != KEY_SENTINEL ? tab.spl[31] : tab.spl[0];
+    const double xs = sk != KEY_SENTINEL ? okey_inv(sk) : 0.0;
+    BR_PH();
+    fr_ic_tail<NT, EMAX>(ic, rw, D, A, ld, row, xk, r2, em, last_in, xs,
+                         reinterpret_cast<uint32_t*>(lds) + fr_ic_xk_words(A), ic_ne BR_PH_ARGS);
   }
   BR_PH();
 }
@@ -298,11 +632,21 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
   uint64_t key[EMAX];
   uint32_t pm = 0, hmin = 0xffffffffu, hmax = 0u;
   int wv = 0;
+  // all loads in flight before the first is consumed (as k_cs_rank_fa)
+  const int ilast = last_in ? t + (EMAX - 1) * NT : (An > 0 ? An - 1 : 0);
+  double xv[EMAX];
+  uint32_t pv = 0;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? t + k * NT : ilast];
+  if (PRES) {
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) pv |= (prow[k < EMAX - 1 ? t + k * NT : ilast] != 0 ? 1u : 0u) << k;
+  }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     const bool in = k < EMAX - 1 || last_in;
-    const double v = in ? x[t + k * NT] : 0.0;
-    const bool p = in && (PRES ? prow[t + k * NT] != 0 : true);
+    const double v = xv[k];
+    const bool p = in && (PRES ? ((pv >> k) & 1u) != 0 : true);
     const bool ok = p && v == v;
     pm |= (uint32_t)p << k;
     key[k] = ok ? okey(v) : KEY_SENTINEL;

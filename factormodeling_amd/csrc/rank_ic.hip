@@ -138,6 +138,20 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   bool over = false;
   uint32_t er[2][ICW_EC / 64];                // this lane's entries (0: none) and their slots
   int es[2][ICW_EC / 64];
+  // the first chunk of the streaming pass (step 2) is in flight during the E-list setup
+  const int An = (int)A;
+  double xq[ICW_PF], rq[ICW_PF][2];
+  uint32_t kq[ICW_PF];
+  auto load = [&](int i0, int s) {
+    const int i = i0 + lane;
+    const bool in = i < An;
+    xq[s] = in ? xf[i] : qnan();
+    kq[s] = in ? (uint32_t)rkf[i] : 0u;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) rq[s][m] = (in && act[m]) ? rr[m][i] : qnan();
+  };
+#pragma unroll
+  for (int s = 0; s < ICW_PF; ++s) load(64 * s, s);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     for (int b = lane; b < nbp; b += 64) T[m][b] = 0u;
@@ -145,23 +159,34 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     for (int q = 0; q < ICW_EC / 64; ++q) { er[m][q] = 0u; es[m][q] = 0; }
   }
   __builtin_amdgcn_wave_barrier();
+  // both lags' lists at once: their (independent) position and rank loads overlap
+  int cl[2];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    if (!act[m]) continue;
-    const int64_t td = s + lagv[m];
-    const int c = npos[td];
-    if (c > ICW_PC) { over = true; continue; }
-    int k = 0;
+  for (int m = 0; m < 2; ++m) cl[m] = act[m] ? npos[s + lagv[m]] : 0;
+  over = cl[0] > ICW_PC || cl[1] > ICW_PC;
+  if (!over) {
+    const int cmax = cl[0] > cl[1] ? cl[0] : cl[1];
+    const int32_t* pp[2] = {pos + (s + (act[0] ? lagv[0] : 0)) * ICW_PC, pos + (s + (act[1] ? lagv[1] : 0)) * ICW_PC};
 #pragma unroll
     for (int q = 0; q < ICW_EC / 64; ++q) {
+      if (64 * q >= cmax) break;              // wave-uniform
       const int j = 64 * q + lane;
-      if (64 * q >= c) break;                 // wave-uniform
-      const uint32_t r2 = j < c ? rkf[pos[td * ICW_PC + j]] : 0u;   // 0: NaN exposure
-      er[m][q] = r2;
-      if (r2) es[m][q] = (int)atomicAdd(&T[m][r2 >> 6], 1u);
-      k += __popcll(__ballot(r2 != 0u));
+      int p[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) p[m] = pp[m][j];                 // unconditional (j < ICW_PC)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) p[m] = j < cl[m] ? p[m] : 0;      // valid positions only
+      uint32_t r2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) r2[m] = (uint32_t)rkf[p[m]];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const uint32_t e = j < cl[m] ? r2[m] : 0u;                  // 0: NaN exposure / no entry
+        er[m][q] = e;
+        if (e) es[m][q] = (int)atomicAdd(&T[m][e >> 6], 1u);
+        ne[m] += __popcll(__ballot(e != 0u));
+      }
     }
-    ne[m] = k;
   }
   if (over) {                                 // > ICW_PC NaN returns: the workgroup kernel takes the row
     if (lane == 0) {
@@ -216,22 +241,9 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int q = 0; q < 6; ++q) sm[m][q] = 0.0;
-  const int An = (int)A;
   // software pipeline, ICW_PF chunks deep: the loads of chunks i+1..i+ICW_PF are in flight
   // while chunk i is reduced (one wave per row: without it every chunk waits a full HBM
-  // latency and only other waves hide it)
-  double xq[ICW_PF], rq[ICW_PF][2];
-  uint32_t kq[ICW_PF];
-  auto load = [&](int i0, int s) {
-    const int i = i0 + lane;
-    const bool in = i < An;
-    xq[s] = in ? xf[i] : qnan();
-    kq[s] = in ? (uint32_t)rkf[i] : 0u;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) rq[s][m] = (in && act[m]) ? rr[m][i] : qnan();
-  };
-#pragma unroll
-  for (int s = 0; s < ICW_PF; ++s) load(64 * s, s);
+  // latency and only other waves hide it); the first ICW_PF were issued before step 1
   for (int i0 = 0; i0 < An; i0 += 64) {
     const double x = xq[0];
     const uint32_t rk = kq[0];
@@ -372,6 +384,103 @@ fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R,
     const unsigned g = (unsigned)std::min<int64_t>(F * D, list_grid);
     FMX_HIP(hipLaunchKernel(kl, dim3(g), dim3(nt), args, 0, st));
   }
+  return FMX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// The rank pass with the daily IC fused in (k_cs_rank_fa<..., IC>): cs_rank + cs_winsor
+// (Yr, Yw set) or the ranks alone (both NULL: C5's IC rank pass), plus the two lags' IC
+// records of every row, in one launch; the ranks never go to HBM.  Rows with more than
+// FR_IC_EC NaN returns for a lag write their doubled ranks to RK and go through
+// k_ic_ranked_list afterwards.
+
+// NaN-return bits of every date: bits[d][w] bit b = R[d][32 w + b] is NaN (one wave per 64
+// assets, ballot)
+__global__ void __launch_bounds__(256)
+k_nan_bits(const double* __restrict__ R, int64_t A, int64_t ld, int64_t nw, uint32_t* __restrict__ bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (i0 >= nw * 32) return;                  // whole waves
+  const int64_t d = blockIdx.y, i = i0 + lane;
+  const bool nan = i < A && !(R[d * ld + i] == R[d * ld + i]);
+  const uint64_t b = __ballot(nan);
+  if (lane == 0) {
+    bits[d * nw + (i0 >> 5)] = (uint32_t)b;
+    bits[d * nw + (i0 >> 5) + 1] = (uint32_t)(b >> 32);
+  }
+}
+
+// Moment anchor of every date: its first non-NaN return (0 if none), one wave per date
+__global__ void __launch_bounds__(64)
+k_ret_anchor(const double* __restrict__ R, int64_t A, int64_t ld, double* __restrict__ rsh) {
+  const int lane = threadIdx.x;
+  const double* r = R + (int64_t)blockIdx.x * ld;
+  double v = 0.0;
+  for (int64_t i0 = 0; i0 < A; i0 += 64) {
+    const double x = i0 + lane < A ? r[i0 + lane] : qnan();
+    const uint64_t b = __ballot(x == x);
+    if (b) {
+      v = fr_readlane_d(x, __ffsll((unsigned long long)b) - 1);
+      break;
+    }
+  }
+  if (lane == 0) rsh[blockIdx.x] = v;
+}
+
+static int64_t nanb_words(int64_t A) { return (A + 63) / 64 * 2; }
+
+// work (int32 units): rsh [D] doubles, NaN bits [D][nw], overflow list [1 + F*D]
+int64_t rank_ic_work_len(int64_t F, int64_t D, int64_t A) { return 2 * D + D * nanb_words(A) + 1 + F * D; }
+
+template <int NT, int E> constexpr auto kcrwi = k_cs_rank_fa<NT, E, false, true, true>;
+template <int NT, int E> constexpr auto kcri = k_cs_rank_fa<NT, E, false, false, true>;
+
+fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const double* R, int64_t F, int64_t D,
+                                int64_t A, int64_t ld, double qlo, double qhi, const int32_t* lags, int n_lags,
+                                fmx_rank2_t* RK, int32_t* work, double* out, hipStream_t st) {
+  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
+  // the rank phase's keys / counters, then (IC tail) the exposures + E tables + partials
+  const size_t lds_fr = std::max<size_t>({(size_t)A * 8, (size_t)FR_CS_WORDS * 4, (size_t)fr_ic_lds_bytes(A, nt_fa)});
+  const int E = br_emax(A, nt_fa);
+  const void* k = E < 0 ? nullptr : (Yr ? FMX_EMAX_TABLE(kcrwi)(nt_fa, E) : FMX_EMAX_TABLE(kcri)(nt_fa, E));
+  const void* kl = FMX_EMAX_TABLE(k_ic_ranked_list)(1024, br_emax(A, 1024));
+  if (!k || !kl || !lds_fits(k, lds_fr)) {
+    set_error("fmx_cs_rank_winsor_ic: rows of A <= 16384 assets");
+    return FMX_ERR_UNSUPPORTED;
+  }
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  const int64_t nw = nanb_words(A);
+  double* rsh = reinterpret_cast<double*>(work);              // work: 8-byte aligned device memory
+  uint32_t* nanb = reinterpret_cast<uint32_t*>(work + 2 * D);
+  int32_t* ovf = work + 2 * D + D * nw;
+  k_nan_bits<<<dim3((unsigned)ceil_div(nw, 8), (unsigned)D), 256, 0, st>>>(R, A, ld, nw, nanb);
+  FMX_LAUNCH_CHECK("k_nan_bits");
+  k_ret_anchor<<<(unsigned)D, 64, 0, st>>>(R, A, ld, rsh);
+  FMX_LAUNCH_CHECK("k_ret_anchor");
+  int L0 = lags[0], L1 = n_lags > 1 ? lags[1] : 0, NL = n_lags;
+  k_ic_empty<<<(unsigned)F, 64, 0, st>>>(out, F, D, L0, L1, NL);
+  FMX_LAUNCH_CHECK("k_ic_empty");
+  FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
+  FrIc ic{R, nanb, rsh, F, nw, L0, L1, NL, out, ovf, RK};
+  int method = FMX_RANK_AVERAGE;
+  const uint8_t* present = nullptr;
+  fmx_rank2_t* RKrow = nullptr;
+  void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic};
+  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  static const int list_grid = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return 2 * std::max(cus, 1);
+  }();
+  const fmx_rank2_t* RKc = RK;
+  void* largs[] = {(void*)&X, (void*)&RKc, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,
+                   (void*)&L1, (void*)&NL, (void*)&out, (void*)&ovf};
+  const unsigned g = (unsigned)std::min<int64_t>(F * D, list_grid);
+  FMX_HIP(hipLaunchKernel(kl, dim3(g), dim3(1024), largs, 0, st));
   return FMX_OK;
 }
 

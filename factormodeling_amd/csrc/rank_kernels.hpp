@@ -27,6 +27,8 @@ static __device__ unsigned long long br_phase_acc[32];
     ++br_ph_i;                                                                         \
   } while (0)
 #define BR_PH_ROW() br_ph_i = 0
+#define BR_PH_PARAMS , uint64_t &br_ph_t, int &br_ph_i     // phase state into a device helper
+#define BR_PH_ARGS , br_ph_t, br_ph_i
 #define BR_PHASE_EXPORT(NAME)                                                          \
   extern "C" int NAME(unsigned long long* out) {                                       \
     unsigned long long z[32] = {};                                                     \
@@ -37,6 +39,8 @@ static __device__ unsigned long long br_phase_acc[32];
 #define BR_PH_INIT (void)0
 #define BR_PH() (void)0
 #define BR_PH_ROW() (void)0
+#define BR_PH_PARAMS
+#define BR_PH_ARGS
 #define BR_PHASE_EXPORT(NAME)
 #endif
 

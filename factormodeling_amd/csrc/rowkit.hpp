@@ -333,5 +333,9 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
 fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R, int64_t F, int64_t D, int64_t A,
                         int64_t ld, const int32_t* lags_host, int n_lags, double* out, int32_t* work, hipStream_t st);
 int64_t ic_ranked_work_len(int64_t F, int64_t D);
+fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const double* R, int64_t F, int64_t D,
+                                int64_t A, int64_t ld, double qlo, double qhi, const int32_t* lags, int n_lags,
+                                fmx_rank2_t* RK, int32_t* work, double* out, hipStream_t st);
+int64_t rank_ic_work_len(int64_t F, int64_t D, int64_t A);
 
 }  // namespace fmx

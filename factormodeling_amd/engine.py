@@ -189,6 +189,36 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
     return Yr, Yw
 
 
+def cs_rank_winsor_ic(X, R, lags=(1, 2), qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, ranks_only=False,
+                      rank2=None):
+    """cs_rank(average) + cs_winsor(qlo, qhi) and the daily IC records of the same rows in
+    ONE pass (fmx_cs_rank_winsor_ic): returns (Yrank, Ywinsor, daily [L][4][F][D]);
+    ``ranks_only``: no operator outputs (the IC's rank pass alone; Yrank = Ywinsor = None).
+    ``rank2``: int16 [F][D][A] scratch for rows with long NaN-return lists (allocated when
+    None).  Dense rows, A <= 16384, one or two lags."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if tuple(R.shape) != (D, A) or R.dtype != F64 or not R.is_contiguous() or R.device != X.device:
+        raise _lib.FmxError("R must be a contiguous float64 [D][A] tensor on X's device")
+    if len(lags) not in (1, 2):
+        raise _lib.FmxError("cs_rank_winsor_ic: one or two lags")
+    Yr = Yw = None
+    if not ranks_only:
+        Yr, Yw = _out(X, out_rank), _out(X, out_winsor)
+    if rank2 is None:
+        rank2 = torch.empty((F, D, A), dtype=RANK2_DTYPE, device=X.device)
+    elif rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+        raise _lib.FmxError("rank2 must be a contiguous int16 [F][D][A] tensor")
+    lag_h = (ctypes.c_int32 * len(lags))(*[int(v) for v in lags])
+    n = int(_lib.load().fmx_rank_ic_work_len(F, D, A))
+    work = _workspace(X.device, n)
+    out = torch.empty((len(lags), 4, F, D), dtype=F64, device=X.device)
+    call("fmx_cs_rank_winsor_ic", ptr(X), ptr(Yr), ptr(Yw), ptr(R), F, D, A, A, float(qlo), float(qhi),
+         ctypes.cast(lag_h, ctypes.c_void_p), len(lags), ptr(rank2), ptr(work), n, ptr(out), stream_ptr())
+    return Yr, Yw, out
+
+
 def cs_rank2(X, rank2=None):
     """Doubled average ranks only (fmx_cs_rank2): the rank pass ``ic_daily(..., rank2=)``
     starts from when no operator output of the rows is wanted (dense rows, A <= 16384)."""

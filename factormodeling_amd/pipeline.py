@@ -288,6 +288,19 @@ class EngineBackend:
         """The doubled ranks alone (no operator output): the IC's rank pass."""
         E.cs_rank2(X, rank2)
 
+    # the daily IC fused into the rank pass (fmx_cs_rank_winsor_ic: the ranks never leave
+    # the CU).  Off by default: at C2 it measured 37.4 ms against 21.1 + 8.8 ms for the rank
+    # pass + k_ic_wave pair (the IC tail lengthens every row's barrier chain at the 3 rows
+    # per CU the LDS admits).  FMX_FUSED_IC=1 selects it (A/B)
+    fused_ic = os.environ.get("FMX_FUSED_IC", "0") == "1"
+
+    @staticmethod
+    def cs_rank_winsor_ic(X, R, lags, outs, rank2):
+        """cs_rank + cs_winsor into ``outs`` (None: ranks only) and the daily IC records."""
+        if outs is None:
+            return E.cs_rank_winsor_ic(X, R, lags, ranks_only=True, rank2=rank2)[2]
+        return E.cs_rank_winsor_ic(X, R, lags, 0.01, 0.99, outs[0], outs[1], rank2=rank2)[2]
+
     def op(self, kind, op, w, X, out):
         if kind == "ts":
             return E.ts(op, X, w, None, out=out)
@@ -408,7 +421,12 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
             if rk is None or tuple(rk.shape) != tuple(X.shape):
                 rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=X.device)
             side["rank2"] = rk
-            be.cs_rank_winsor(X, outs, rank2=rk)
+            if _fused_ic(be, side):
+                # ... inside the same pass: the daily IC records of every row
+                side["daily"] = be.cs_rank_winsor_ic(X, side["R"], side["lags"], outs, rk)
+                name = "cs_rank_winsor_ic"
+            else:
+                be.cs_rank_winsor(X, outs, rank2=rk)
         else:
             be.cs_rank_winsor(X, outs)
     else:
@@ -421,6 +439,12 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
     if collect is not None:
         for o, y in zip(ops, outs):
             collect[_op_key(*o)] = y[:, own].clone()
+
+
+def _fused_ic(be, side):
+    """The backend fuses the daily IC into the rank pass for this step's lags."""
+    return (getattr(be, "fused_ic", False) and hasattr(be, "cs_rank_winsor_ic") and side.get("R") is not None
+            and 1 <= len(side.get("lags") or ()) <= 2)
 
 
 def _ev(timers):
@@ -469,7 +493,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     """One pass of the hot path.  Returns (selected weights [J][F] (every rank holds the
     full result; None without selection), kept factor list (None without the Gram)).
     ``collect`` (tests) receives intermediate results."""
-    side = {"rank2_buf": getattr(sp, "rank2", None)}   # filled as "rank2" when this step ranks X
+    # "rank2" is filled when this step ranks X; "daily" when the IC ran inside the rank pass
+    side = {"rank2_buf": getattr(sp, "rank2", None), "R": sp.R, "lags": tuple(cfg.ic_lags)}
     streams = None
     early = not cfg.streams
     t0 = _ev(timers)
@@ -513,18 +538,27 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         run_ret_ops(sp, cfg, timers, be, collect)
     if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
             and sp.A <= getattr(be, "rank_pass_max_a", 0)):
-        # no operator ranked X this step: one ranks-only pass feeds the wave IC
+        # no operator ranked X this step: one ranks-only pass feeds the IC (inside the pass
+        # when the backend fuses it, else the wave IC from the ranks)
         t0 = _ev(timers)
         rk = getattr(sp, "rank2", None)
         if rk is None:
             rk = torch.empty(sp.X.shape, dtype=E.RANK2_DTYPE, device=sp.X.device)
-        be.cs_rank2(sp.X, rk)
         side["rank2"] = rk
-        _rec(timers, "rank2", t0)
+        if _fused_ic(be, side):
+            side["daily"] = be.cs_rank_winsor_ic(sp.X, sp.R, side["lags"], None, rk)
+            _rec(timers, "rank_ic", t0)
+        else:
+            be.cs_rank2(sp.X, rk)
+            _rec(timers, "rank2", t0)
     # daily IC for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
     lags = tuple(cfg.ic_lags)
-    if side.get("rank2") is not None:
+    if side.get("daily") is not None:
+        sp.rank2 = side["rank2"]
+        daily = side["daily"][:, :, :, sp.halo:]                        # made by the rank pass
+        t0 = None
+    elif side.get("rank2") is not None:
         sp.rank2 = side["rank2"]                                        # buffer reused next step
         daily = be.ic_daily(sp.X, sp.R, lags, rank2=sp.rank2)[:, :, :, sp.halo:]
     else:

@@ -206,6 +206,21 @@ int64_t fmx_ic_ranked_work_len(int64_t F, int64_t D);
 fmx_status fmx_ic_daily_ranked(const double* X, const fmx_rank2_t* rank2, const double* R, int64_t F, int64_t D,
                                int64_t A, int64_t ld, const int32_t* lags, int32_t n_lags, int32_t* work,
                                int64_t work_len, double* out, void* stream);
+/* cs_rank(method='average') + cs_winsor (operations.py:54-68) AND the daily IC of the same
+ * rows (factor_selector.py:36-48: pearsonr, pearsonr(rankdata), beta of the pairs
+ * (X[f][t-L], R[t])) in ONE pass: each row's ranks feed its IC records inside the
+ * workgroup, so no rank panel is written or re-read.  Yrank / Ywinsor: both set (outputs
+ * bit-identical to fmx_cs_rank_winsor) or both NULL (the IC's rank pass alone).  lags: HOST
+ * int32[n_lags], n_lags 1 or 2; out as fmx_ic_daily (records agree with it to ~1e-15
+ * relative, pair counts exactly).  rank2: device fmx_rank2_t [F][D][ld] scratch, written
+ * only for rows with > 256 NaN returns (finished by the workgroup kernel of
+ * fmx_ic_daily_ranked).  work: device int32 of fmx_rank_ic_work_len(F, D, A).  Dense rows
+ * (no presence mask), A <= 16384. */
+int64_t fmx_rank_ic_work_len(int64_t F, int64_t D, int64_t A);
+fmx_status fmx_cs_rank_winsor_ic(const double* X, double* Yrank, double* Ywinsor, const double* R, int64_t F,
+                                 int64_t D, int64_t A, int64_t ld, double qlo, double qhi, const int32_t* lags,
+                                 int32_t n_lags, fmx_rank2_t* rank2, int32_t* work, int64_t work_len, double* out,
+                                 void* stream);
 /* Window summaries of one lag's daily stats [4][F][D] over J date windows [d0, d1).
  * out: [J][F][8] = IC, IC_IR, rank_IC, rank_IC_IR, tstat, n_beta, pct_pos, n_days. */
 fmx_status fmx_ic_window(const double* daily, int64_t F, int64_t D, const int32_t* d0_dev, const int32_t* d1_dev,

@@ -149,6 +149,40 @@ def test_ic_ranked_matches_standalone_ic(dev, A, r_nan, lags):
     np.testing.assert_allclose(got[:, 1:], ref[:, 1:], rtol=1e-12, atol=1e-14, equal_nan=True)
 
 
+@pytest.mark.parametrize("A,r_nan", [(1, 0.0), (9, 0.1), (300, 0.005), (1000, 0.05), (5000, 0.005), (5000, 0.045),
+                                     (5000, 0.07), (10000, 0.005), (12000, 0.015), (16384, 0.004)])
+@pytest.mark.parametrize("lags", [(1, 2), (1,), (0, 2)])
+def test_rank_winsor_ic_fused_matches_standalone(dev, A, r_nan, lags):
+    """The IC fused into the rank pass (fmx_cs_rank_winsor_ic: the ranks never leave the
+    workgroup; rows with > 256 NaN returns through the workgroup list kernel) == the
+    standalone IC: pair counts exactly, statistics to 1e-12 relative; the rank / winsor
+    outputs bit-identical to fmx_cs_rank_winsor; the ranks-only variant gives the same
+    records."""
+    import torch
+    import factormodeling_amd.engine as E
+    F, D = (3, 9) if A <= 5000 else (2, 7)
+    X, R = _ic_case(A + 3 * len(lags), F, D, A, r_nan)
+    if A == 1:
+        X[0, 2, 0] = np.nan
+    Xt, Rt = torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev)
+    yr, yw, got = E.cs_rank_winsor_ic(Xt, Rt, lags)
+    _, _, got2 = E.cs_rank_winsor_ic(Xt, Rt, lags, ranks_only=True)
+    rr, rw = E.cs_rank_winsor(Xt, 0.01, 0.99)
+    assert np.array_equal(yr.cpu().numpy(), rr.cpu().numpy(), equal_nan=True)
+    assert np.array_equal(yw.cpu().numpy(), rw.cpu().numpy(), equal_nan=True)
+    got, got2 = got.cpu().numpy(), got2.cpu().numpy()
+    assert np.array_equal(got, got2, equal_nan=True)
+    if A <= 12288:
+        ref = E.ic_daily(Xt, Rt, lags).cpu().numpy()
+    else:                                      # beyond the standalone kernels: the ranked IC
+        rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
+        E.cs_rank_winsor(Xt, 0.01, 0.99, rank2=rk)
+        ref = E.ic_daily(Xt, Rt, lags, rank2=rk).cpu().numpy()
+    assert np.array_equal(got[:, 0], ref[:, 0])
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    np.testing.assert_allclose(got[:, 1:], ref[:, 1:], rtol=1e-12, atol=1e-14, equal_nan=True)
+
+
 def test_rank2_is_doubled_average_rank(dev):
     import torch
     from scipy.stats import rankdata
@@ -190,17 +224,29 @@ def test_step_ranked_ic_matches_unranked(dev):
     class Unranked(PL.EngineBackend):
         ranked_ic_max_a = 0
 
+    class Fused(PL.EngineBackend):
+        fused_ic = True
+
+    class Unfused(PL.EngineBackend):
+        fused_ic = False
+
     cfg = PL.StepConfig(sel_window=10)
     out = []
-    for be in (PL.ENGINE, Unranked()):
+    for be in (Fused(), Unfused(), Unranked()):
         sp = PL.ShardedPanel(60, 400, 6, 0, 1, dev, seed=3, halo=cfg.halo)
         col = {}
-        w, kept = PL.run_step(sp, cfg, be=be, collect=col)
-        out.append((col["daily"].cpu().numpy(), w.cpu().numpy(), kept, getattr(sp, "rank2", None) is not None))
-    assert out[0][3] and not out[1][3]
-    np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-12, atol=1e-14, equal_nan=True)
-    assert np.array_equal(out[0][1], out[1][1])
-    assert list(out[0][2]) == list(out[1][2])
+        timers = []
+        w, kept = PL.run_step(sp, cfg, be=be, collect=col, timers=timers)
+        names = {n for n, _, _ in timers}
+        out.append((col["daily"].cpu().numpy(), w.cpu().numpy(), kept, getattr(sp, "rank2", None) is not None,
+                    names))
+    assert out[0][3] and out[1][3] and not out[2][3]
+    assert "cs_rank_winsor_ic" in out[0][4] and "ic_daily" not in out[0][4]      # fused: no IC stage
+    assert "ic_daily" in out[1][4]
+    for o in out[1:]:
+        np.testing.assert_allclose(out[0][0], o[0], rtol=1e-12, atol=1e-14, equal_nan=True)
+        assert np.array_equal(out[0][1], o[1])
+        assert list(out[0][2]) == list(o[2])
 
 
 def test_ic_ranked_long_rows_vs_oracle(dev):

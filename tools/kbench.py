@@ -89,6 +89,9 @@ OPS = {
     "cs_rw": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"]), 24),
     "cs_rw_rk": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"], rank2=_rank2(X)), 26),
     "ic_ranked": (lambda X, R, Y: E.ic_daily(X, R, (1, 2), rank2=_rank2(X)), 10),
+    "cs_rw_ic": (lambda X, R, Y: E.cs_rank_winsor_ic(X, R, (1, 2), 0.01, 0.99, Y, _set_outs(X)["mean"],
+                                                     rank2=_RK.setdefault("rk", torch.empty(X.shape, dtype=E.RANK2_DTYPE,
+                                                                                            device=X.device))), 24),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
     "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
     "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
