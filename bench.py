@@ -13,8 +13,9 @@ an IC all-gather and a Gram all-reduce over RCCL.
 Other workloads (BASELINE configs[3], [4]; parity cases, not the driver's line):
   c4  2,520 x 3,000 x 2,000 factor zoo: daily IC + full-sample metrics for the pruning
       order, the 2,000 x 2,000 correlation Gram (fp64 MFMA, chunked by date) + greedy prune;
-  c5  2,520 x 10,000 x 500: ts_corr(x, R, 60) and ts_std(60) over factor chunks, daily IC
-      lags 1-2, 60-day window metrics, icir_top weights, weighted composite (zscore).
+  c5  2,520 x 10,000 x 500: ts_corr(x, R, 60) over factor chunks feeding the feature panel
+      sign(ts_corr) * x / ts_std(x, 60); its daily IC lags 1-2, 60-day window metrics,
+      icir_top weights and the weighted composite (zscore) of the feature panel.
 
 Rank 0 prints one JSON line (driver contract) with ``roofline`` (dominant kernel,
 HIP-event timed inside the timed steps), ``cpu_baseline`` (the numpy oracle port on a
@@ -58,6 +59,8 @@ def bytes_per_unit(stage, F, ranked=False):
         return 8.0 + 16.0 / F
     if kind == "rank2":              # ranks-only pass: X once + the u16 doubled ranks
         return 10.0
+    if stage.startswith("ret:cvf"):     # C5 feature: X (+ the leaving value) and ts_corr in, F out
+        return 24.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
         return 16.0
     if kind == "ic_daily":              # X once (+ its u16 ranks when ranked) + two R rows
@@ -99,7 +102,7 @@ def pmc_traffic(stage, dims):
 WORKLOAD_DIMS = {"c2": (2520, 5000, 200), "c4": (2520, 3000, 2000), "c5": (2520, 10000, 500)}
 WORKLOAD_NAME = {"c2": "C2 ops+IC+icir_top+corr-prune",
                  "c4": "C4 wide zoo: IC order + 2000x2000 corr Gram (fp64 MFMA) + greedy prune",
-                 "c5": "C5 ts_corr/ts_std(60) + rolling-IC icir_top + weighted composite"}
+                 "c5": "C5 ts_corr/ts_std(60) feature -> its daily IC -> icir_top -> weighted composite"}
 
 
 def parse():

@@ -503,6 +503,51 @@ k_ts_rl(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t
   }
 }
 
+// C5's feature (builder-defined): the rolling-W ts_std of each column feeding
+// a sign-aligned, volatility-scaled exposure
+//     F = sign(C) * (x / ts_std(x, W))      (ts_std == 0 -> NaN, as ts_zscore's replace(0, NaN))
+// where C = ts_corr(x, R, W) was computed for the same rows (np.sign semantics: +-0 -> +0,
+// NaN -> NaN).  The same Welford machine and operation order as k_ts_rl<STD>, so the
+// std is bit-identical to fmx_ts_op(STD) and F to the numpy restatement.
+template <int PF>
+__global__ void __launch_bounds__(256)
+k_ts_cvf_rl(const double* __restrict__ X, const double* __restrict__ C, double* __restrict__ Y, int64_t F,
+            int64_t D, int64_t A, int64_t ld, int W) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  const double* cc = C + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  ColState c;
+  c.init();
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double v[PF], o[PF], cv[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      v[q] = d < D ? x[d * ld] : 0.0;
+      o[q] = (d < D && d >= W) ? x[(d - W) * ld] : 0.0;
+      cv[q] = d < D ? __builtin_nontemporal_load(cc + d * ld) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      const double vv = v[q];
+      if (c.first) { c.ss.init(vv); c.ms.init(vv); c.vs.init(vv); c.first = false; }
+      if (c.i >= W) c.vs.remove(o[q]);
+      c.vs.add(vv);
+      double sd = zsqrt(c.vs.var(W, 1));
+      if (sd == 0.0) sd = qnan();
+      const double cq = cv[q];
+      const double sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
+      __builtin_nontemporal_store(sg * (vv / sd), y + d * ld);
+      c.i += 1;
+    }
+  }
+}
+
 // ts_corr on dense panels with the leaving values re-read (k_ts_corr's ring is 2W x 64
 // doubles of LDS per wave).  Same operation order as k_ts_corr: bit-identical.
 template <int PF>
@@ -924,6 +969,20 @@ extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* O
   void* args[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,
                   (void*)&y_fstride, (void*)&W, (void*)&present};
   return launch_ring((const void*)k_ts_corr, grid, lds, as_stream(stream), args);
+}
+
+extern "C" fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, double* Y, int64_t F, int64_t D,
+                                              int64_t A, int64_t ld, int32_t window, void* stream) {
+  FMX_ARG(X && C && Y, "null panel");
+  FMX_ARG(Y != X && Y != C, "output must not alias the inputs");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(window >= 1, "window must be >= 1");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  int W = window;
+  void* args[] = {(void*)&X, (void*)&C, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W};
+  FMX_HIP(hipLaunchKernel((const void*)k_ts_cvf_rl<8>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args, 0,
+                          as_stream(stream)));
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_ts_regression(const double* Yv, const double* Xv, const uint8_t* valid, double* Out,

@@ -93,6 +93,21 @@ def ts_corr(X, Ycol, window: int, present=None, out=None):
     return out
 
 
+def corr_vol_feature(X, C, window: int, out=None):
+    """C5's feature sign(C) * (X / ts_std(X, window)) (fmx_ts_corr_vol_feature); C is
+    ts_corr(X, R, window) of the same rows (same shape as X)."""
+    X = as3(X)
+    _check_panel(X)
+    C = as3(C)
+    _check_panel(C, "C")
+    if C.shape != X.shape:
+        raise _lib.FmxError("C must be shaped like X")
+    F, D, A = X.shape
+    out = _out(X, out)
+    call("fmx_ts_corr_vol_feature", ptr(X), ptr(C), ptr(out), F, D, A, A, int(window), stream_ptr())
+    return out
+
+
 def ts_regression(Yv, Xv, valid, window: int, rettype: int):
     D, A = Yv.shape
     if tuple(Xv.shape) != (D, A) or tuple(valid.shape) != (D, A) or valid.dtype != torch.uint8:

@@ -50,7 +50,10 @@ class StepConfig:
     select: bool = True        # rolling-window metrics + icir_top per processed day
     gram: bool = True          # correlation Gram + greedy pruning
     prune_top_x: object = "top_x"   # None: prune the whole ordered zoo
-    ret_ops: list = field(default_factory=list)   # [(op, window)] vs returns: ("corr", 60), ("std", 60)
+    # [(op, window)] vs returns: ("corr", 60), ("std", 60) into scratch; ("corr_vol", 60): the
+    # feature panel sign(ts_corr(x, R, w)) * x / ts_std(x, w) that the IC, the selection and
+    # the composite then run on (C5: ts_corr / ts_std feeding the IC-weighted composite)
+    ret_ops: list = field(default_factory=list)
     factor_chunk: int = 0      # ret_ops run over chunks of this many factors (memory)
     composite: object = None   # "zscore" | "rank": weighted composite of the day's selection
     names: object = None       # factor names (composite suffix / prefix rules)
@@ -82,7 +85,7 @@ def workload_config(name):
     if name == "c4":
         return StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None)
     if name == "c5":
-        return StepConfig(ops=[], ic_lags=(1, 2), select=True, gram=False, ret_ops=[("corr", 60), ("std", 60)],
+        return StepConfig(ops=[], ic_lags=(1, 2), select=True, gram=False, ret_ops=[("corr_vol", 60)],
                           factor_chunk=100, composite="zscore", rank_pass=True)
     raise ValueError(f"unknown workload {name!r}")
 
@@ -347,6 +350,10 @@ class EngineBackend:
     def ts_corr_into(X, R, w, out):
         E.ts_corr(X, R, w, out=out)
 
+    @staticmethod
+    def corr_vol_feature(X, C, w, out):
+        E.corr_vol_feature(X, C, w, out=out)
+
     wcomp = staticmethod(E.wcomp)
     ic_daily = staticmethod(E.ic_daily)
     ic_window = staticmethod(E.ic_window)
@@ -464,29 +471,49 @@ def _rec(timers, name, t0):
 
 
 def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
-    """Operators against the returns (C5: ts_corr(x, R, w), plus ts_std(x, w)) over factor
-    chunks of ``cfg.factor_chunk`` into reused buffers (a full-size output per operator
-    would not fit next to a 100 GB panel)."""
+    """Operators against the returns over factor chunks of ``cfg.factor_chunk`` (a
+    full-size output per operator would not fit next to a 100 GB panel): ("corr", w) /
+    ("std", w) write reused chunk buffers; ("corr_vol", w) -- C5 -- writes ts_corr(x, R, w)
+    of the chunk into a chunk buffer and then the chunk of the feature panel sp.feature =
+    sign(ts_corr) * x / ts_std(x, w) (fmx_ts_corr_vol_feature), which the rest of the step
+    runs on."""
     F = sp.X.shape[0]
     fc = cfg.factor_chunk or F
+    n = min(fc, F)
     bufs = getattr(sp, "ret_bufs", None)
-    if bufs is None or bufs[0].shape[0] != min(fc, F):
-        bufs = [torch.empty((min(fc, F),) + tuple(sp.X.shape[1:]), dtype=sp.X.dtype, device=sp.X.device)
+    if bufs is None or bufs[0].shape[0] != n or len(bufs) != len(cfg.ret_ops):
+        bufs = [torch.empty((n,) + tuple(sp.X.shape[1:]), dtype=sp.X.dtype, device=sp.X.device)
                 for _ in cfg.ret_ops]
         sp.ret_bufs = bufs
+    if any(op == "corr_vol" for op, _ in cfg.ret_ops) and getattr(sp, "feature", None) is None:
+        sp.feature = torch.empty_like(sp.X)
     for f0 in range(0, F, fc):
         f1 = min(F, f0 + fc)
         Xc = sp.X[f0:f1]
         for (op, w), buf in zip(cfg.ret_ops, bufs):
             out = buf[: f1 - f0]
             t0 = _ev(timers)
-            if op == "corr":
+            if op in ("corr", "corr_vol"):
                 be.ts_corr_into(Xc, sp.R, w, out)
             else:
                 be.op("ts", op, w, Xc, out)
-            _rec(timers, f"ret:{op}:{w}", t0)
+            _rec(timers, f"ret:{'corr' if op == 'corr_vol' else op}:{w}", t0)
             if collect is not None:
-                collect.setdefault(f"ret:{op}:{w}", []).append(out[:, sp.halo:].clone())
+                collect.setdefault(f"ret:{'corr' if op == 'corr_vol' else op}:{w}", []).append(out[:, sp.halo:].clone())
+            if op == "corr_vol":
+                t0 = _ev(timers)
+                be.corr_vol_feature(Xc, out, w, sp.feature[f0:f1])
+                _rec(timers, f"ret:cvf:{w}", t0)
+    if collect is not None and getattr(sp, "feature", None) is not None:
+        collect["feature"] = sp.feature[:, sp.halo:].clone()
+
+
+def _step_panel(sp, cfg):
+    """The panel the IC, the selection and the composite run on: the C5 feature panel
+    when the step builds one, else the factor panel itself."""
+    if any(op == "corr_vol" for op, _ in cfg.ret_ops):
+        return sp.feature
+    return sp.X
 
 
 def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=None):
@@ -536,6 +563,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
             _rec(timers, "gram", t0)
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
+    Xs = _step_panel(sp, cfg)
     if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
             and sp.A <= getattr(be, "rank_pass_max_a", 0)):
         # no operator ranked X this step: one ranks-only pass feeds the IC (inside the pass
@@ -543,13 +571,13 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         t0 = _ev(timers)
         rk = getattr(sp, "rank2", None)
         if rk is None:
-            rk = torch.empty(sp.X.shape, dtype=E.RANK2_DTYPE, device=sp.X.device)
+            rk = torch.empty(Xs.shape, dtype=E.RANK2_DTYPE, device=Xs.device)
         side["rank2"] = rk
         if _fused_ic(be, side):
-            side["daily"] = be.cs_rank_winsor_ic(sp.X, sp.R, side["lags"], None, rk)
+            side["daily"] = be.cs_rank_winsor_ic(Xs, sp.R, side["lags"], None, rk)
             _rec(timers, "rank_ic", t0)
         else:
-            be.cs_rank2(sp.X, rk)
+            be.cs_rank2(Xs, rk)
             _rec(timers, "rank2", t0)
     # daily IC for owned dates (halo provides the lagged rows)
     t0 = _ev(timers)
@@ -560,9 +588,9 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         t0 = None
     elif side.get("rank2") is not None:
         sp.rank2 = side["rank2"]                                        # buffer reused next step
-        daily = be.ic_daily(sp.X, sp.R, lags, rank2=sp.rank2)[:, :, :, sp.halo:]
+        daily = be.ic_daily(Xs, sp.R, lags, rank2=sp.rank2)[:, :, :, sp.halo:]
     else:
-        daily = be.ic_daily(sp.X, sp.R, lags)[:, :, :, sp.halo:]      # [L][4][F][own]
+        daily = be.ic_daily(Xs, sp.R, lags)[:, :, :, sp.halo:]        # [L][4][F][own]
     _rec(timers, "ic_daily", t0)
     t0 = _ev(timers)
     L = len(lags)
@@ -588,7 +616,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     comp = None
     if cfg.composite and w is not None:
         t0 = _ev(timers)
-        comp = weighted_composite_step(sp, cfg, w, be)
+        comp = weighted_composite_step(sp, cfg, w, be, Xs)
         _rec(timers, "composite", t0)
     if streams is not None:                       # join
         main = torch.cuda.current_stream(sp.X.device)
@@ -647,11 +675,13 @@ def gram_total(sp, be, part):
     return a, b
 
 
-def weighted_composite_step(sp, cfg, w, be=ENGINE):
+def weighted_composite_step(sp, cfg, w, be=ENGINE, X=None):
     """weighted_composite_factor (composite_factor.py:220-342) of each processed day's
-    selection over this rank's owned dates: the day's selected columns, pooled suffix
-    percentiles, prefix proxies, group weights, z-score / rank, demeaning."""
+    selection over this rank's owned dates of ``X`` (default the factor panel; C5: its
+    feature panel): the day's selected columns, pooled suffix percentiles, prefix proxies,
+    group weights, z-score / rank, demeaning."""
     from .composite_factor import weighted_plan
+    X = sp.X if X is None else X
     W = cfg.sel_window
     D = w.shape[0] + W + 1
     proc = np.arange(W, D - 1)
@@ -659,8 +689,10 @@ def weighted_composite_step(sp, cfg, w, be=ENGINE):
     own = (proc >= sp.d_lo) & (proc < sp.d_hi)
     pdate = np.where(own, local, -1)
     names = cfg.names or factor_names(sp.F)
+    if hasattr(be, "weighted_composite"):               # the oracle (tests)
+        return be.weighted_composite(X, names, pdate, w, cfg.composite)
     plan = weighted_plan(pdate, w.cpu().numpy(), names)
-    return be.wcomp(sp.X, plan, cfg.composite)
+    return be.wcomp(X, plan, cfg.composite)
 
 
 def ordered_sum(T, comm):

@@ -138,6 +138,13 @@ fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int64_t F, int6
 fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                                const uint8_t* present, double* stats, void* stream);
 
+/* C5's feature (builder-defined; BASELINE configs[4] "60-day rolling ts_corr/ts_std feeding
+ * IC-weighted composite"): Y = sign(C) * (X / ts_std(X, window)) per column, ts_std ==
+ * 0 -> NaN, C = fmx_ts_corr(X, R, window) of the same rows (np.sign semantics).  The std is
+ * pandas' rolling Welford (operations.py:14-15), bit-identical to fmx_ts_op(FMX_TS_STD).
+ * Dense panels. */
+fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, double* Y, int64_t F, int64_t D, int64_t A,
+                                   int64_t ld, int32_t window, void* stream);
 /* cs_zscore (Yz) and market_neutralize (Yn) of the same rows from ONE set of moments
  * (operations.py:77-78, :171-182); optional stats[F][D][2] = (mean, std ddof=0).  Outputs
  * bit-identical to fmx_cs_moment of each op; distinct from X and each other. */

@@ -178,6 +178,19 @@ def ts_corr(x, y, window, present=None):
     return _expand(f(xc, yc), rows, x.shape)
 
 
+def corr_vol_feature(x, y, window):
+    """C5's feature (builder-defined; no reference counterpart): the 60-day
+    ts_corr / ts_std of BASELINE configs[4] feeding the composite as
+    ``sign(ts_corr(x, y, w)) * (x / ts_std(x, w).replace(0, NaN))`` -- each factor
+    sign-aligned with its own recent return correlation and scaled by its own rolling
+    volatility (ts_std = operations.py:14-15, the replace(0, NaN) guard of ts_zscore
+    :18-21).  np.sign: +-0 -> +0, NaN -> NaN."""
+    s = ts_std(x, window)
+    c = ts_corr(x, y, window)
+    with np.errstate(all="ignore"):
+        return np.sign(c) * (x / np.where(s == 0, np.nan, s))
+
+
 def _roll_count(ok, window):
     c = np.cumsum(ok.astype(np.int64), axis=0)
     out = c.copy()

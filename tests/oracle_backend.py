@@ -28,6 +28,29 @@ class OracleBackend:
             out[f] = torch.from_numpy(r)
         return out
 
+    def ts_corr_into(self, X, R, w, out):
+        x, r = X.numpy(), R.numpy()
+        for f in range(x.shape[0]):
+            out[f] = torch.from_numpy(O.ts_corr(x[f], r, w))
+        return out
+
+    def corr_vol_feature(self, X, C, w, out):
+        """sign(C) * x / ts_std(x, w) with C = the step's ts_corr (oracle.ops.corr_vol_feature)."""
+        x, c = X.numpy(), C.numpy()
+        for f in range(x.shape[0]):
+            s = O.ts_std(x[f], w)
+            with np.errstate(all="ignore"):
+                out[f] = torch.from_numpy(np.sign(c[f]) * (x[f] / np.where(s == 0, np.nan, s)))
+        return out
+
+    def weighted_composite(self, X, names, pdate, w, method):
+        """weighted_composite_factor of each processed day's selection (owned dates only)."""
+        import oracle.composite as OC
+        own = np.asarray(pdate) >= 0
+        W = w.numpy() if isinstance(w, torch.Tensor) else np.asarray(w)
+        out = OC.weighted_composite_factor(X.numpy(), names, list(np.asarray(pdate)[own]), W[own], method)
+        return torch.from_numpy(out)
+
     def ic_daily(self, X, R, lags):
         x, r = X.numpy(), R.numpy()
         Fn, Dn, _ = x.shape
