@@ -36,6 +36,13 @@ __device__ __forceinline__ int fr_lane() {
   asm volatile("" : "+v"(l));
   return l;
 }
+// A value the compiler must treat as unknown at this point: per-element addresses are
+// recomputed at their use (one VALU op) instead of being kept live across the kernel --
+// the register allocator spills such address vectors rather than rematerialise them.
+__device__ __forceinline__ int fr_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 __device__ __forceinline__ int fr_xor_i(int v, int m, int lane) {
   return __builtin_amdgcn_ds_bpermute((lane ^ m) << 2, v);
 }
@@ -395,13 +402,15 @@ __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* ke
 // Bucket ids of all EMAX keys of a thread, searched in lockstep groups of up to 5 (that
 // many independent LDS reads in flight per step) and branch-free; sentinel keys get
 // bucket `dummy`.
-template <int K, int EMAX>
+// G: group size (fewer keys in flight for register-tight launches, e.g. 1024-thread rows
+// at 64 VGPRs)
+template <int K, int EMAX, int G = 4>
 __device__ __forceinline__ void fr_bucket_all(const FrTab& T, const uint64_t* key, int* b, int dummy) {
-  if constexpr (EMAX <= 5) {
+  if constexpr (EMAX <= G + 1) {
     fr_bucket_grp<K, EMAX>(T, key, b, dummy);
   } else {
-    fr_bucket_grp<K, 4>(T, key, b, dummy);
-    fr_bucket_all<K, EMAX - 4>(T, key + 4, b + 4, dummy);
+    fr_bucket_grp<K, G>(T, key, b, dummy);
+    fr_bucket_all<K, EMAX - G, G>(T, key + G, b + G, dummy);
   }
 }
 

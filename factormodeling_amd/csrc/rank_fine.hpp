@@ -369,7 +369,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   double xv[EMAX];
   uint32_t pv = 0;
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? t + k * NT : ilast];
+  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? fr_opaque(t) + k * NT : ilast];
   if (PRES) {
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) pv |= (prow[k < EMAX - 1 ? t + k * NT : ilast] != 0 ? 1u : 0u) << k;
@@ -415,17 +415,17 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (Y) {                                  // Y == NULL: doubled ranks only (fmx_cs_rank2)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) y[t + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+        if (k < EMAX - 1 || last_in) y[fr_opaque(t) + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
     }
     if (RK) {                                 // nv == 0 or a single-row date (rank 1)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) RK[row * ld + t + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
+        if (k < EMAX - 1 || last_in) RK[row * ld + fr_opaque(t) + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
     }
     if (WQ) {                                 // nv < 5: winsor is the identity
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) Y2[row * ld + t + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+        if (k < EMAX - 1 || last_in) Y2[row * ld + fr_opaque(t) + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
     }
     if constexpr (IC) {                       // < 3 pairs: empty records (n = 0, or 1 on a one-asset row)
       if (t == 0) {
@@ -450,7 +450,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   int sl[EMAX];                               // slot | bucket << PK_BSHIFT, then start | len << 16
   {
     int bb[EMAX];
-    fr_bucket_all<K, EMAX>(tab, key, bb, DUMMY);
+    fr_bucket_all<K, EMAX, (NT >= 1024 ? 2 : 4)>(tab, key, bb, DUMMY);
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) sl[k] = (int)fr_cnt_add(cnt, bb[k]) | (bb[k] << PK_BSHIFT);
   }
@@ -528,9 +528,10 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     else if (method == FMX_RANK_MAX) r = (double)(less + eq);
     else r = (double)less + (double)(eq + 1) / 2.0;
     // write-once outputs: nontemporal stores
-    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den, y + t + k * NT);
+    const int ia = fr_opaque(t) + k * NT;       // recomputed here, not kept from the loads
+    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den, y + ia);
     if (RK) __builtin_nontemporal_store((fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1)),
-                                        RK + row * ld + t + k * NT);
+                                        RK + row * ld + ia);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -573,7 +574,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
       double o = v;
       if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
-      __builtin_nontemporal_store((PRES && !((pm >> k) & 1)) ? qnan() : o, y2 + t + k * NT);
+      __builtin_nontemporal_store((PRES && !((pm >> k) & 1)) ? qnan() : o, y2 + fr_opaque(t) + k * NT);
     }
   }
   if constexpr (IC) {
