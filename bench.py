@@ -202,7 +202,24 @@ REFERENCE_CPU = {
     "source": "SURVEY.md §6: C1 (500x1000x20 ops+IC+select+composite) measured 307.4 s in the build container; "
               "C2 extrapolated from measured C2 slices: 8 operators ~3,200 s + winsor ~3,500 s + ts_decay ~6,100 s "
               "+ ts_rank ~159,000 s + single_factor_metrics ~1,700 s + FactorSelector ~57,500 s = ~2.3e5 s",
+    "reconciliation": "BASELINE.md's 'about 4e4 f·a·d/s' (~17 h) sums the per-operator, single_factor_metrics and "
+                      "FactorSelector extrapolations without ts_rank(10) (~44 h: pandas rolling.apply with a Python "
+                      "callback per element) and the cs_winsor / ts_decay slices; the C2 operator set includes all "
+                      "three, so the full extrapolation is ~2.3e5 s = 1.1e4 f·a·d/s",
 }
+
+
+def host_cpu():
+    """(logical CPUs of this host, CPU model string) for the cpu_baseline record."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return os.cpu_count(), model
 
 
 def spawn_ranks(n):
@@ -252,7 +269,11 @@ def main():
         # before this process initialises the GPU: the port's workers are spawned children
         dims0 = WORKLOAD_DIMS[args.workload]
         rate, cores, sample = cpu_baseline(args.dates or dims0[0], args.assets or dims0[1], args.cpu_workers)
-        cpu = {"value": rate, "unit": "factor·asset·days/s", "cores": cores, "kind": "port", "sample": sample}
+        ncpu, model = host_cpu()
+        # cores: the worker processes the port actually used (one thread each); host_cpus:
+        # the logical CPUs of the machine (the GPU box exposes many more than its CPU share)
+        cpu = {"value": rate, "unit": "factor·asset·days/s", "cores": cores, "kind": "port", "sample": sample,
+               "host_cpus": ncpu, "cpu_model": model}
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)

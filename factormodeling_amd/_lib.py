@@ -34,6 +34,9 @@ SIGNATURES = {
     "fmx_cs_rank_winsor": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp, c_vp],
     "fmx_cs_rank_sorted": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp],
     "fmx_cs_rank_sorted_work_bytes": [c_i64, c_i64, c_i64],
+    "fmx_cs_quantile_sorted": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp, c_i64, c_vp],
+    "fmx_group_rank_sorted": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    "fmx_group_rank_sorted_work_bytes": [c_i64, c_i64, c_i64],
     "fmx_cs_rank2": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
@@ -81,7 +84,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
-             "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
+             "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_group_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
              "fmx_debug_exact_fold": None}
 
 # constants mirrored from include/fmx.h

@@ -164,6 +164,7 @@ def cs_zscore_neutralize(X, out_z=None, out_n=None, present=None, with_stats=Fal
 
 
 RANKED_IC_MAX_A = 16384
+FINE_RANK_MAX_A = 16384     # fine-bucket rank / quantile kernels; longer rows are sorted in HBM
 RANK2_DTYPE = torch.int16   # fmx_rank2_t: doubled ranks <= 2A as uint16 bit patterns
 BITONIC_RANK_MAX_A = 8192   # fmx_cs_rank's LDS bitonic path (methods first / dense)
 _WORK = {}
@@ -199,6 +200,11 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
     if rank2 is not None:
         if rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
             raise _lib.FmxError("rank2 must be a contiguous int16 (bit pattern uint16) [F][D][A] tensor")
+    if A > FINE_RANK_MAX_A and rank2 is None:
+        # rows past the fused kernel: both operators from rows sorted in HBM
+        cs_rank(X, "average", present, out=Yr)
+        cs_quantile_op("winsor", X, qlo, qhi, present, out=Yw)
+        return Yr, Yw
     call("fmx_cs_rank_winsor", ptr(X), ptr(Yr), ptr(Yw), F, D, A, A, float(qlo), float(qhi), ptr(present),
          ptr(rank2), stream_ptr())
     return Yr, Yw
@@ -256,8 +262,9 @@ def cs_rank(X, method="average", present=None, out=None):
     if method not in RANK:
         raise ValueError(f"unknown rank method {method!r}")
     Y = _out(X, out)
-    if method in ("first", "dense") and A > BITONIC_RANK_MAX_A:
-        # rows past the LDS bitonic kernel: sorted in HBM (fmx_cs_rank_sorted)
+    if (method in ("first", "dense") and A > BITONIC_RANK_MAX_A) or A > FINE_RANK_MAX_A:
+        # rows past the LDS bitonic kernel (first / dense) or the fine-bucket kernels (the
+        # other methods): sorted in HBM (fmx_cs_rank_sorted)
         nb = int(_lib.load().fmx_cs_rank_sorted_work_bytes(F, D, A))
         work, wb = _workspace_bytes(X.device, nb)
         call("fmx_cs_rank_sorted", ptr(X), ptr(Y), F, D, A, A, RANK[method], ptr(present), ptr(work), wb,
@@ -273,6 +280,13 @@ def cs_quantile_op(kind: str, X, qlo: float, qhi: float, present=None, out=None)
     F, D, A = X.shape
     _check_present(present, D, A)
     Y = _out(X, out)
+    if A > FINE_RANK_MAX_A:
+        # past the fine-bucket quantile kernels: order statistics of rows sorted in HBM
+        nb = int(_lib.load().fmx_cs_rank_sorted_work_bytes(F, D, A))
+        work, wb = _workspace_bytes(X.device, nb)
+        call("fmx_cs_quantile_sorted", 0 if kind == "winsor" else 1, ptr(X), ptr(Y), F, D, A, A, float(qlo),
+             float(qhi), ptr(present), ptr(work), wb, stream_ptr())
+        return Y
     fn = "fmx_cs_winsor" if kind == "winsor" else "fmx_cs_filter_center"
     call(fn, ptr(X), ptr(Y), F, D, A, A, float(qlo), float(qhi), ptr(present), stream_ptr())
     return Y
@@ -286,16 +300,26 @@ def group_op(op: str, X, G, ngroups: int, method="average", present=None):
     if G.dtype != torch.int32 or tuple(G.shape) != (D, A):
         raise _lib.FmxError("G must be int32 [D][A]")
     if op == "rank" and A > 4096 and ngroups > 0:
-        # codes outside [0, ngroups) belong to no group (the kernel sorts them past the last
-        # boundary); clamp the index so the count never writes out of bounds
-        ok = (G >= 0) & (G < ngroups)
-        if present is not None:
-            ok &= present != 0
-        cnt = torch.zeros((D, ngroups), dtype=torch.int32, device=G.device)
-        cnt.scatter_add_(1, G.clamp(0, ngroups - 1).long(), ok.int())
-        if int(cnt.max()) > 8192:
-            raise _lib.FmxError("group_rank_normalized on rows > 4096 assets sorts each group in LDS: "
-                                "at most 8192 members per (date, group)")
+        big = A > FINE_RANK_MAX_A
+        if not big:
+            # codes outside [0, ngroups) belong to no group (the kernel sorts them past the
+            # last boundary); clamp the index so the count never writes out of bounds
+            ok = (G >= 0) & (G < ngroups)
+            if present is not None:
+                ok &= present != 0
+            cnt = torch.zeros((D, ngroups), dtype=torch.int32, device=G.device)
+            cnt.scatter_add_(1, G.clamp(0, ngroups - 1).long(), ok.int())
+            big = int(cnt.max()) > 8192          # the per-group LDS sort takes <= 8192 members
+        if big:
+            # rows sorted by (group, value) in HBM (fmx_group_rank_sorted): any group size
+            Y = torch.empty_like(X)
+            nb = int(_lib.load().fmx_group_rank_sorted_work_bytes(F, D, A))
+            work, wb = _workspace_bytes(X.device, nb)
+            call("fmx_group_rank_sorted", ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method],
+                 ptr(present), ptr(work), wb, stream_ptr())
+            return Y
+    elif A > FINE_RANK_MAX_A:
+        raise _lib.FmxError(f"group_{op} on rows of more than {FINE_RANK_MAX_A} assets is not supported")
     Y = torch.empty_like(X)
     call("fmx_group_op", GROUP[op], ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method], ptr(present),
          stream_ptr())

@@ -163,13 +163,27 @@ fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t
 fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
                               int64_t ld, double qlo, double qhi, const uint8_t* present, fmx_rank2_t* rank2,
                               void* stream);
-/* cs_rank(method='first' | 'dense') for any row length (A <= 65535): rows sorted in HBM
- * (rocPRIM segmented radix sort of (value key, asset) pairs, stable), then one workgroup
- * per row scatters the ranks.  fmx_cs_rank takes these methods up to A = 8192 (LDS
- * bitonic); this entry has no such limit.  work: fmx_cs_rank_sorted_work_bytes(F, D, A). */
+/* cs_rank, every method, for any row length (A <= 65535): rows sorted in HBM (rocPRIM
+ * segmented radix sort of (value key, asset) pairs, stable), then one wave per row walks
+ * its tie runs and scatters the ranks.  fmx_cs_rank takes 'first' / 'dense' up to A = 8192
+ * (LDS bitonic) and the other methods up to 16384 (fine buckets); this entry has no such
+ * limit.  work: fmx_cs_rank_sorted_work_bytes(F, D, A). */
 fmx_status fmx_cs_rank_sorted(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, int32_t method,
                               const uint8_t* present, void* work, int64_t work_bytes, void* stream);
 int64_t fmx_cs_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
+/* cs_winsor (op 0) / cs_filter_center (op 1) (operations.py:64-75) for any row length
+ * (A <= 65535): the numpy 'linear' order statistics read off the sorted rows.  work:
+ * fmx_cs_rank_sorted_work_bytes(F, D, A). */
+fmx_status fmx_cs_quantile_sorted(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                  double qlo, double qhi, const uint8_t* present, void* work, int64_t work_bytes,
+                                  void* stream);
+/* group_rank_normalized (operations.py:152-168) for any group size and row length (A <=
+ * 65535): rows sorted by (group, value) in two stable passes.  G, ngroups as fmx_group_op;
+ * methods average / min / max / first / dense.  work: fmx_group_rank_sorted_work_bytes. */
+fmx_status fmx_group_rank_sorted(const double* X, const int32_t* G, double* Y, int64_t F, int64_t D, int64_t A,
+                                 int64_t ld, int32_t ngroups, int32_t method, const uint8_t* present, void* work,
+                                 int64_t work_bytes, void* stream);
+int64_t fmx_group_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
 /* Only the doubled average ranks of fmx_cs_rank_winsor (rank2 [F][D][ld] fmx_rank2_t, A <=
  * 16384): the rank pass of a daily IC over raw factors (fmx_ic_daily_ranked) when no
  * operator output of the same rows is wanted (factor_selector.py:36-48's rankdata). */
