@@ -53,13 +53,15 @@ SIGNATURES = {
                               c_i64, c_vp, c_vp],
     "fmx_ic_window": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "fmx_select_icir_top": [c_vp, c_i64, c_i64, c_i32, c_dbl, c_i32, c_vp, c_vp, c_vp],
-    "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_zscore_exposures": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_corr_prune_windows": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32,
                                c_dbl, c_dbl, c_i32, c_vp, c_vp, c_i64, c_vp],
     "fmx_corr_prune_windows_work_bytes": [c_i64, c_i64, c_i64, c_i32, c_vp],
-    "fmx_zscore_exposures_range": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_zscore_exposures_range": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_gram": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     "fmx_gram_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i32],
+    "fmx_gram_direct": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
+    "fmx_gram_direct_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     "fmx_gram_fused_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "fmx_gram_exact": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
@@ -82,7 +84,7 @@ SIGNATURES = {
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64,
+_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64, "fmx_gram_direct_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
              "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_group_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
              "fmx_debug_exact_fold": None}

@@ -68,30 +68,39 @@ static GramPlan gram_plan(int64_t F, int64_t A, int64_t d0, int64_t d1, bool mas
 // per-date z-score of one (f, d) row; builder spec: mean/std(ddof=0) over non-NaN,
 // NaN -> 0, sigma in {0, NaN} -> whole row 0 and M = 0.  M is written as bf16 0/1.
 // Dates [d0, d0 + gridDim.x) of X [F][D][ld] into Z / M [F][Dout][ld] (Dout = the range
-// length: a date chunk of a panel too large to materialise Z for all dates).
+// length: a date chunk of a panel too large to materialise Z for all dates).  stats
+// ([F][D] (mean, sd) of fmx_cs_moment_stats: numpy-pairwise, the oracle's moments bit for
+// bit) when given; else block sums here (a constant row's sigma can then round to a tiny
+// nonzero where numpy's is exactly 0).
 __global__ void __launch_bounds__(256)
-k_zscore_exposures(const double* __restrict__ X, double* __restrict__ Z, uint16_t* __restrict__ M, int64_t D,
-                   int64_t A, int64_t ld, int64_t d0, int64_t Dout) {
+k_zscore_exposures(const double* __restrict__ X, const double* __restrict__ stats, double* __restrict__ Z,
+                   uint16_t* __restrict__ M, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t Dout) {
   __shared__ double dscr[16];
   const int64_t d = blockIdx.x, f = blockIdx.y;
   const double* x = X + (f * D + d0 + d) * ld;
   double* z = Z + (f * Dout + d) * ld;
   uint16_t* m = M + (f * Dout + d) * ld;
-  double s = 0.0, c = 0.0;
-  for (int64_t a = threadIdx.x; a < A; a += 256) {
-    double v = x[a];
-    if (v == v) { s += v; c += 1.0; }
+  double mean, sd;
+  if (stats) {
+    mean = stats[2 * (f * D + d0 + d)];
+    sd = stats[2 * (f * D + d0 + d) + 1];
+  } else {
+    double s = 0.0, c = 0.0;
+    for (int64_t a = threadIdx.x; a < A; a += 256) {
+      double v = x[a];
+      if (v == v) { s += v; c += 1.0; }
+    }
+    s = block_sum<256>(s, dscr);
+    c = block_sum<256>(c, dscr);
+    mean = c > 0 ? s / c : qnan();
+    double q = 0.0;
+    for (int64_t a = threadIdx.x; a < A; a += 256) {
+      double v = x[a];
+      if (v == v) q += (v - mean) * (v - mean);
+    }
+    q = block_sum<256>(q, dscr);
+    sd = c > 0 ? sqrt(q / c) : qnan();
   }
-  s = block_sum<256>(s, dscr);
-  c = block_sum<256>(c, dscr);
-  const double mean = c > 0 ? s / c : qnan();
-  double q = 0.0;
-  for (int64_t a = threadIdx.x; a < A; a += 256) {
-    double v = x[a];
-    if (v == v) q += (v - mean) * (v - mean);
-  }
-  q = block_sum<256>(q, dscr);
-  const double sd = c > 0 ? sqrt(q / c) : qnan();
   const bool ok = sd > 0.0;
   for (int64_t a = threadIdx.x; a < ld; a += 256) {
     double v = a < A ? x[a] : qnan();
@@ -102,7 +111,8 @@ k_zscore_exposures(const double* __restrict__ X, double* __restrict__ Z, uint16_
 }
 
 // ---------------------------------------------------------------------------------------
-template <bool VEC>
+// PADNAN: cells past the row / panel read as NaN (the direct Gram z-scores them to 0)
+template <bool VEC, bool PADNAN = false>
 __device__ __forceinline__ void load_chunk(const double* __restrict__ row, bool rowok, int64_t a0, int lc,
                                            int64_t A, double* r) {
   if (VEC && rowok && a0 + lc + 8 <= A) {
@@ -117,7 +127,7 @@ __device__ __forceinline__ void load_chunk(const double* __restrict__ row, bool 
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       int64_t a = a0 + lc + u;
-      r[u] = (rowok && a < A) ? row[a] : 0.0;
+      r[u] = (rowok && a < A) ? row[a] : (PADNAN ? qnan() : 0.0);
     }
   }
 }
@@ -1116,24 +1126,25 @@ extern "C" void fmx_debug_exact_fold(const double* x, int64_t n, int64_t* limbs_
   if (value_out) *value_out = ex_value(acc);
 }
 
-extern "C" fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
-                                           int64_t ld, void* stream) {
+extern "C" fmx_status fmx_zscore_exposures(const double* X, const double* stats, double* Z, uint16_t* M, int64_t F,
+                                           int64_t D, int64_t A, int64_t ld, void* stream) {
   FMX_ARG(X && Z && M, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
   if (F == 0 || D == 0) return FMX_OK;
-  k_zscore_exposures<<<dim3((unsigned)D, (unsigned)F), 256, 0, as_stream(stream)>>>(X, Z, M, D, A, ld, 0, D);
+  k_zscore_exposures<<<dim3((unsigned)D, (unsigned)F), 256, 0, as_stream(stream)>>>(X, stats, Z, M, D, A, ld, 0, D);
   FMX_LAUNCH_CHECK("k_zscore_exposures");
   return FMX_OK;
 }
 
-extern "C" fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D,
-                                                 int64_t A, int64_t ld, int64_t d0, int64_t d1, void* stream) {
+extern "C" fmx_status fmx_zscore_exposures_range(const double* X, const double* stats, double* Z, uint16_t* M,
+                                                 int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
+                                                 void* stream) {
   FMX_ARG(X && Z && M, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d0 <= d1 && d1 <= D, "bad dims");
   if (F == 0 || d1 == d0) return FMX_OK;
   FMX_ARG(F <= 65535, "too many factors");
-  k_zscore_exposures<<<dim3((unsigned)(d1 - d0), (unsigned)F), 256, 0, as_stream(stream)>>>(X, Z, M, D, A, ld, d0,
-                                                                                            d1 - d0);
+  k_zscore_exposures<<<dim3((unsigned)(d1 - d0), (unsigned)F), 256, 0, as_stream(stream)>>>(X, stats, Z, M, D, A,
+                                                                                            ld, d0, d1 - d0);
   FMX_LAUNCH_CHECK("k_zscore_exposures");
   return FMX_OK;
 }
@@ -1183,6 +1194,248 @@ extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, do
   fmx_status e = gram_run(Z, false, G, F, D, A, ld, d0, d1, accumulate, part, st);
   if (e || !with_mask) return e;
   return gram_run(M, true, N, F, D, A, ld, d0, d1, accumulate, part, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// Wide-panel Gram straight from the panel (fmx_gram_direct, C4's 2000 x 2000): no Z / M
+// materialisation.  The row moments are the caller's fmx_cs_moment_stats (numpy pairwise
+// mean / std ddof=0: the oracle's z-score spec bit-for-bit, as the F <= 256 Gram uses).
+// (1) k_valid_bits: validity bits (x not NaN, sigma > 0), factor-major [F][nd][nwd];
+// (2) k_gram_f64x: k_gram_f64 with the z-score applied while a chunk is staged (X + the
+// row's (mean, sd) instead of Z); (3) k_gram_popc_fm: N = M M^T as AND + popcount of the
+// bits (exact integers), 64 x 64 tiles, 4 x 4 pairs per thread.
+__global__ void __launch_bounds__(256)
+k_valid_bits(const double* __restrict__ X, const double* __restrict__ stats, int64_t D, int64_t A, int64_t ld,
+             int64_t d0, int64_t nd, int64_t nwd, uint32_t* __restrict__ bits) {
+  const int64_t d = blockIdx.x, f = blockIdx.y;
+  const double* x = X + (f * D + d0 + d) * ld;
+  const bool ok = stats[2 * (f * D + d0 + d) + 1] > 0.0;     // sigma in {0, NaN}: no valid cell
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* b = bits + (f * nd + d) * nwd;
+  for (int64_t i0 = (int64_t)wid * 64; i0 < nwd * 32; i0 += 256) {
+    const int64_t i = i0 + lane;
+    const double v = x[i < A ? i : 0];
+    const uint64_t bal = __ballot(ok && i < A && v == v);
+    if (lane == 0) {
+      b[i0 >> 5] = (uint32_t)bal;
+      if ((i0 >> 5) + 1 < nwd) b[(i0 >> 5) + 1] = (uint32_t)(bal >> 32);
+    }
+  }
+}
+
+// k_gram_f64 over the raw panel: the chunk's rows are z-scored as they are staged
+// (valid = sd > 0 and x not NaN: (x - mean) / sd, else 0 -- k_zscore_exposures' values).
+template <bool VEC>
+__global__ void __launch_bounds__(512)
+k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
+            int64_t d0, int64_t d1, int64_t dates_per_slice, int nb, int64_t ntile, double* __restrict__ part) {
+  extern __shared__ double gsm[];             // [2][As | Bs], GT * GKP doubles each
+  const int64_t tile = blockIdx.x, slice = blockIdx.y;
+  int ti, tj;
+  upper_tile((int)tile, nb, ti, tj);
+  const int i0 = ti * GT, j0 = tj * GT;
+  const int64_t ds = d0 + slice * dates_per_slice;
+  const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  dbl4 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const int lr = tid >> 2, lc = (tid & 3) * 8;
+  const bool rowA = (i0 + lr) < F, rowB = (j0 + lr) < F;
+  const int64_t nch = (A + GK - 1) / GK;
+  const int64_t total = (de - ds) * nch;
+  double ra[8], rb[8];
+  double2 sa, sb;                             // (mean, sd) of the staged rows' date
+  auto issue = [&](int64_t c) {
+    const int64_t d = ds + c / nch, a0 = (c % nch) * GK;
+    load_chunk<VEC, true>(X + ((int64_t)(i0 + lr) * D + d) * ld, rowA, a0, lc, A, ra);
+    load_chunk<VEC, true>(X + ((int64_t)(j0 + lr) * D + d) * ld, rowB, a0, lc, A, rb);
+    const double2* z = reinterpret_cast<const double2*>(zst);   // stats [F][D] (mean, sd)
+    sa = rowA ? z[(int64_t)(i0 + lr) * D + d] : make_double2(0.0, 0.0);
+    sb = rowB ? z[(int64_t)(j0 + lr) * D + d] : make_double2(0.0, 0.0);
+  };
+  auto stage = [&](int buf) {
+    double* As = gsm + buf * 2 * GT * GKP;
+    double* Bs = As + GT * GKP;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double va = ra[u], vb = rb[u];
+      As[lr * GKP + lc + u] = (sa.y > 0.0 && va == va) ? (va - sa.x) / sa.y : 0.0;
+      Bs[lr * GKP + lc + u] = (sb.y > 0.0 && vb == vb) ? (vb - sb.x) / sb.y : 0.0;
+    }
+  };
+  if (total > 0) {
+    issue(0);
+    stage(0);
+  }
+  __syncthreads();
+  if (total > 1) issue(1);
+  for (int64_t c = 0; c < total; ++c) {
+    const double* As = gsm + (c & 1) * 2 * GT * GKP;
+    const double* Bs = As + GT * GKP;
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      const int k = kk + (lane >> 4);
+      double af[4], bf[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) af[m] = As[(wr * 64 + m * 16 + (lane & 15)) * GKP + k];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) bf[n] = Bs[(wc * 32 + n * 16 + (lane & 15)) * GKP + k];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+    }
+    if (c + 1 < total) stage((int)((c + 1) & 1));
+    __syncthreads();
+    if (c + 2 < total) issue(c + 2);
+  }
+  double* p = part + (slice * ntile + tile) * (GT * GT);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;
+        const int col = wc * 32 + n * 16 + (lane & 15);
+        p[row * GT + col] = acc[m][n][r];
+      }
+}
+
+// N[i][j] = sum over the bit words of popcount(bits[i] & bits[j]), factor-major bits
+// [F][nw]: one workgroup per (64 x 64 upper tile, word range); 64-word chunks of the tile's
+// 2 x 64 rows staged in LDS; thread (ty, tx) owns rows ty + 16 r and columns tx + 16 c
+// (4 x 4 pairs: 8 LDS words per 16 AND/popcounts).  64-bit atomics into ncnt[F][F].
+constexpr int PF_T = 64, PF_W = 64;
+__global__ void __launch_bounds__(256)
+k_gram_popc_fm(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t wps,
+               unsigned long long* __restrict__ ncnt) {
+  __shared__ uint32_t Ai[PF_T][PF_W + 1], Bj[PF_T][PF_W + 1];
+  const int tid = threadIdx.x;
+  int tt = blockIdx.x, ti = 0;
+  const int T = (int)((F + PF_T - 1) / PF_T);
+  while (tt >= T - ti) { tt -= T - ti; ++ti; }
+  const int I0 = ti * PF_T, J0 = (ti + tt) * PF_T;
+  const int64_t w0 = (int64_t)blockIdx.y * wps, w1 = min<int64_t>(nw, w0 + wps);
+  const int ty = tid >> 4, tx = tid & 15;
+  unsigned acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = 0u;
+  for (int64_t wc = w0; wc < w1; wc += PF_W) {
+    for (int q = tid; q < PF_T * PF_W; q += 256) {
+      const int r = q / PF_W, w = q % PF_W;     // row-contiguous words: coalesced
+      const bool in = wc + w < w1;
+      Ai[r][w] = (in && I0 + r < F) ? bits[(int64_t)(I0 + r) * nw + wc + w] : 0u;
+      Bj[r][w] = (in && J0 + r < F) ? bits[(int64_t)(J0 + r) * nw + wc + w] : 0u;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int w = 0; w < PF_W; ++w) {
+      uint32_t a[4], b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = Ai[ty + 16 * r][w];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[c] = Bj[tx + 16 * c][w];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] += __popc(a[r] & b[c]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int gi = I0 + ty + 16 * r, gj = J0 + tx + 16 * c;
+      if (gi < F && gj < F && gi <= gj && acc[r][c]) atomicAdd(&ncnt[(int64_t)gi * F + gj], (unsigned long long)acc[r][c]);
+    }
+}
+
+// N from the counts (upper triangle incl. the diagonal), mirrored; accumulate adds to N
+__global__ void k_gram_counts(const unsigned long long* __restrict__ ncnt, int64_t F, double* __restrict__ N,
+                              int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= F * F) return;
+  const int64_t i = e / F, j = e % F;
+  if (i > j) return;
+  double n = (double)ncnt[e];
+  if (accumulate) n += N[i * F + j];
+  N[i * F + j] = n;
+  N[j * F + i] = n;
+}
+
+struct DirectPlan {
+  GramPlan g;
+  int64_t nd, nwd, nw;
+  int64_t bits_bytes() const { return SmallPlan::align256((int64_t)sizeof(uint32_t) * F * nw); }
+  int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * g.part_elems()); }
+  int64_t cnt_bytes() const { return (int64_t)sizeof(unsigned long long) * F * F; }
+  int64_t bytes() const { return bits_bytes() + part_bytes() + cnt_bytes(); }
+  int64_t F;
+};
+static DirectPlan direct_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
+  DirectPlan p;
+  p.F = F;
+  p.g = gram_plan(F, A, d0, d1, false);
+  p.nd = d1 - d0;
+  p.nwd = ceil_div(A, (int64_t)32);
+  p.nw = p.nd * p.nwd;
+  return p;
+}
+
+extern "C" int64_t fmx_gram_direct_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
+  (void)D;
+  if (F <= 0 || d1 <= d0) return 0;
+  return direct_plan(F, A, d0, d1).bytes();
+}
+
+extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, double* G, double* N, int64_t F,
+                                      int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate,
+                                      void* work, int64_t work_bytes, void* stream) {
+  FMX_ARG(X && stats && G && N, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
+  FMX_ARG(F <= 65535 && d1 - d0 <= 0x7fffffff, "too many factors / dates");
+  if (F == 0 || d1 == d0) return FMX_OK;
+  const DirectPlan pl = direct_plan(F, A, d0, d1);
+  if (fmx_status e = check_work(work, work_bytes, pl.bytes(), "fmx_gram_direct_work_bytes")) return e;
+  hipStream_t st = as_stream(stream);
+  char* w = static_cast<char*>(work);
+  const double* zst = stats;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(w);
+  double* part = reinterpret_cast<double*>(w + pl.bits_bytes());
+  unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
+  k_valid_bits<<<dim3((unsigned)pl.nd, (unsigned)F), 256, 0, st>>>(X, stats, D, A, ld, d0, pl.nd, pl.nwd, bits);
+  FMX_LAUNCH_CHECK("k_valid_bits");
+  dim3 grid((unsigned)pl.g.ntile, (unsigned)pl.g.nslice);
+  const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64x<true> : (const void*)k_gram_f64x<false>;
+  FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAM_F64_LDS));
+  int nb = pl.g.nb;
+  int64_t dps = pl.g.dps, ntile = pl.g.ntile;
+  void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
+                  (void*)&dps, (void*)&nb, (void*)&ntile, (void*)&part};
+  FMX_HIP(hipLaunchKernel(k, grid, dim3(512), args, GRAM_F64_LDS, st));
+  k_gram_reduce<<<dim3((unsigned)pl.g.ntile, GT * GT / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, pl.g.nb, F,
+                                                                          G, accumulate);
+  FMX_LAUNCH_CHECK("k_gram_reduce");
+  FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
+  const int T = (int)ceil_div(F, (int64_t)PF_T);
+  const int ntp = T * (T + 1) / 2;
+  // >= ~2048 workgroups: the word range is cut into pieces of whole 64-word chunks
+  const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(pl.nw, (int64_t)4 * PF_W), 2048 / ntp + 1));
+  const int64_t wps = ceil_div(ceil_div(pl.nw, nks), (int64_t)PF_W) * PF_W;
+  k_gram_popc_fm<<<dim3((unsigned)ntp, (unsigned)ceil_div(pl.nw, wps)), 256, 0, st>>>(bits, F, pl.nw, wps, ncnt);
+  FMX_LAUNCH_CHECK("k_gram_popc_fm");
+  k_gram_counts<<<(unsigned)ceil_div(F * F, (int64_t)256), 256, 0, st>>>(ncnt, F, N, accumulate);
+  FMX_LAUNCH_CHECK("k_gram_counts");
+  return FMX_OK;
 }
 
 extern "C" int64_t fmx_corr_prune_windows_work_bytes(int64_t F, int64_t D, int64_t J, int32_t window,

@@ -398,13 +398,17 @@ def select_icir_top(metrics, use_rank_icir=True, threshold=0.03, top_x=5):
     return order, w
 
 
-def zscore_exposures(X):
+def zscore_exposures(X, stats=None):
+    """Z (per-date z-score, NaN -> 0, sigma in {0, NaN} -> row 0) and M (bf16 0/1) from
+    the numpy-pairwise row moments of cs_moment_stats (the oracle's, bit for bit)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
+    if stats is None:
+        _, stats = cs_moment_stats("stats", X)
     Z = torch.empty_like(X)
     M = torch.empty(X.shape, dtype=torch.bfloat16, device=X.device)   # 0/1 validity
-    call("fmx_zscore_exposures", ptr(X), ptr(Z), ptr(M), F, D, A, A, stream_ptr())
+    call("fmx_zscore_exposures", ptr(X), ptr(stats), ptr(Z), ptr(M), F, D, A, A, stream_ptr())
     return Z, M
 
 
@@ -494,6 +498,7 @@ def gram_chunked(X, d0=0, d1=None, chunk=None):
     d1 = D if d1 is None else d1
     if chunk is None:
         chunk = max(1, min(d1 - d0, int(GRAM_CHUNK_BYTES // max(1, F * A * 10))))
+    _, stats = cs_moment_stats("stats", X)
     G = torch.zeros((F, F), dtype=F64, device=X.device)
     N = torch.zeros((F, F), dtype=F64, device=X.device)
     Z = M = None
@@ -503,11 +508,42 @@ def gram_chunked(X, d0=0, d1=None, chunk=None):
         if Z is None or Z.shape[1] != n:
             Z = torch.empty((F, n, A), dtype=F64, device=X.device)
             M = torch.empty((F, n, A), dtype=torch.bfloat16, device=X.device)
-        call("fmx_zscore_exposures_range", ptr(X), ptr(Z), ptr(M), F, D, A, A, c0, c1, stream_ptr())
+        call("fmx_zscore_exposures_range", ptr(X), ptr(stats), ptr(Z), ptr(M), F, D, A, A, c0, c1, stream_ptr())
         nb = int(_lib.load().fmx_gram_work_bytes(F, n, A, 0, n, 1))
         work, wb = _workspace_bytes(X.device, nb)
         call("fmx_gram", ptr(Z), ptr(M), ptr(G), ptr(N), F, n, A, A, 0, n, 1, ptr(work), wb, stream_ptr())
     return G, N
+
+
+def gram_direct(X, d0=0, d1=None, stats=None):
+    """G, N over dates [d0, d1) for wide factor sets (F > 256, C4's 2000) straight from
+    the panel (fmx_gram_direct): the z-score (row stats of fmx_cs_moment_stats, computed
+    here unless given) is applied while each tile chunk is staged and N comes from AND +
+    popcount of validity bits -- no Z / M panels in HBM."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    d1 = D if d1 is None else d1
+    if stats is None:
+        _, stats = cs_moment_stats("stats", X)
+    elif tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous():
+        raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
+    G = torch.empty((F, F), dtype=F64, device=X.device)
+    N = torch.empty((F, F), dtype=F64, device=X.device)
+    nb = int(_lib.load().fmx_gram_direct_work_bytes(F, D, A, int(d0), int(d1)))
+    work, wb = _workspace_bytes(X.device, nb)
+    call("fmx_gram_direct", ptr(X), ptr(stats), ptr(G), ptr(N), F, D, A, A, int(d0), int(d1), 0, ptr(work), wb,
+         stream_ptr())
+    return G, N
+
+
+def gram_wide(X, d0=0, d1=None):
+    """The wide (F > 256) Gram: direct from the panel by default; FMX_GRAM_MATERIALIZE=1
+    selects the date-chunked Z / M path (A/B)."""
+    import os
+    if os.environ.get("FMX_GRAM_MATERIALIZE") == "1":
+        return gram_chunked(X, d0, d1)
+    return gram_direct(X, d0, d1)
 
 
 def corr_matrix(X, d0=0, d1=None, stats=None):
@@ -520,7 +556,7 @@ def corr_matrix(X, d0=0, d1=None, stats=None):
             _, stats = cs_moment_stats("stats", X)
         G, N = gram_fused(X, stats, d0, d1)
     else:
-        G, N = gram_chunked(X, d0, d1)
+        G, N = gram_wide(X, d0, d1)
     return torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
 
 

@@ -335,7 +335,7 @@ class EngineBackend:
     @staticmethod
     def corr_gram(X, d0, d1, stats=None, z=None):
         """G, N over dates [d0, d1): fused single pass for F <= 256 (from ``z``, the
-        step's cs_zscore output, when given), else Z/M + tiles."""
+        step's cs_zscore output, when given), else the wide tiles straight from X."""
         if X.shape[0] <= E.FUSED_GRAM_MAX_F:
             # the z input needs the default kernel; the A/B switches take the stats path
             ab = os.environ.get("FMX_GRAM_SINGLE_BUFFER") or os.environ.get("FMX_GRAM_MASK_MFMA")
@@ -344,7 +344,7 @@ class EngineBackend:
             if stats is None:
                 _, stats = E.cs_moment_stats("stats", X)
             return E.gram_fused(X, stats, d0, d1)
-        return E.gram_chunked(X, d0, d1)
+        return E.gram_wide(X, d0, d1)
 
     @staticmethod
     def ts_corr_into(X, R, w, out):

@@ -253,16 +253,27 @@ fmx_status fmx_select_icir_top(const double* metrics, int64_t J, int64_t F, int3
 
 /* ---- factor correlation GEMM (builder-defined) ------------------------ */
 /* Z: per-date z-scored exposures (float64 [F][D][ld], NaN -> 0); M: validity as bf16
- * 0/1 (uint16 bit patterns [F][D][ld]). */
-fmx_status fmx_zscore_exposures(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
-                                int64_t ld, void* stream);
+ * 0/1 (uint16 bit patterns [F][D][ld]).  stats: fmx_cs_moment_stats' [F][D][2] (mean, sd)
+ * -- the oracle's numpy moments bit for bit -- or NULL for in-kernel block sums. */
+fmx_status fmx_zscore_exposures(const double* X, const double* stats, double* Z, uint16_t* M, int64_t F, int64_t D,
+                                int64_t A, int64_t ld, void* stream);
 /* fmx_zscore_exposures for the dates [d0, d1) only: Z / M are [F][d1 - d0][ld] (chunked
  * Gram of a panel whose full Z / M would not fit next to X, e.g. C4 at 121 GB). */
-fmx_status fmx_zscore_exposures_range(const double* X, double* Z, uint16_t* M, int64_t F, int64_t D, int64_t A,
-                                      int64_t ld, int64_t d0, int64_t d1, void* stream);
+fmx_status fmx_zscore_exposures_range(const double* X, const double* stats, double* Z, uint16_t* M, int64_t F,
+                                      int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, void* stream);
 /* G[F][F] (+)= sum_{d in [d0,d1), a} Z[i][d][a] Z[j][d][a] on fp64 MFMA
  * (v_mfma_f64_16x16x4_f64) and N[F][F] (+)= the same sum over M on bf16 MFMA (exact
  * pair counts).  accumulate = 0 overwrites.  M/N may be NULL. */
+/* The wide-panel correlation Gram straight from the raw panel (builder-defined A19, C4's
+ * 2000 x 2000): G = Z^T Z (fp64 MFMA, 128 x 128 tiles) with Z z-scored while each tile
+ * chunk is staged from stats[F][D][2] (fmx_cs_moment_stats: numpy-pairwise mean / std
+ * ddof=0; NaN -> 0, sigma 0 or NaN -> row 0), and N = M^T M as AND + popcount of validity
+ * bits (exact).  No Z / M panels are materialised.  Dates [d0, d1); accumulate adds into
+ * G / N.  work: fmx_gram_direct_work_bytes. */
+int64_t fmx_gram_direct_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1);
+fmx_status fmx_gram_direct(const double* X, const double* stats, double* G, double* N, int64_t F, int64_t D,
+                           int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,
+                           int64_t work_bytes, void* stream);
 fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, double* N, int64_t F, int64_t D, int64_t A,
                     int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work, int64_t work_bytes,
                     void* stream);

@@ -164,6 +164,36 @@ def test_corr_gram_2000_factors_and_prune(dev):
         assert E.greedy_prune(C, order, rho, top) == OG.greedy_prune(Cref, order, rho, top)
 
 
+@pytest.mark.parametrize("F,D,A", [(300, 7, 131), (2000, 4, 96)])
+def test_gram_direct_equals_materialised(dev, F, D, A):
+    """The wide Gram straight from the panel (fmx_gram_direct: z-scored while staged from
+    the numpy-pairwise row stats, N by popcount of validity bits) == the materialised Z / M
+    path to rounding, and == the oracle spec (N exactly, incl. a constant row); a date
+    sub-range."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F + A)
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    X[3, 1] = 0.7                                   # constant row: sigma 0 -> no contribution
+    X[5, 2] = np.nan                                # all-NaN row
+    Xt = torch.as_tensor(X, device=dev)
+    G1, N1 = E.gram_direct(Xt)
+    G0, N0 = E.gram_chunked(Xt)
+    np.testing.assert_allclose(G1.cpu().numpy(), G0.cpu().numpy(), rtol=1e-12, atol=1e-11)
+    assert np.array_equal(N1.cpu().numpy(), N0.cpu().numpy())
+    Z, M = OG.zscore_exposures(X)
+    Mf = M.reshape(F, -1)
+    assert np.array_equal(N1.cpu().numpy(), Mf @ Mf.T)           # exact pair counts (oracle spec)
+    Z, M = OG.zscore_exposures(X[:, 1:3])
+    Mf = M.reshape(F, -1).astype(np.float64)
+    G2, N2 = E.gram_direct(Xt, 1, 3)
+    assert np.array_equal(N2.cpu().numpy(), Mf @ Mf.T)
+    Zf = Z.reshape(F, -1)
+    np.testing.assert_allclose(G2.cpu().numpy(), Zf @ Zf.T, rtol=1e-10, atol=1e-10)
+
+
 def test_corr_prune_selector_through_factor_selector(dev):
     import oracle.metrics as OM
     from factormodeling_amd.factor_selector import FactorSelector
