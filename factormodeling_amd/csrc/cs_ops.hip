@@ -160,6 +160,25 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
 // and occupancy is set by registers.  Requires L <= CSR_NT / 8 leaves of <= 128 elements.
 constexpr int CSR_NT = 512;
 constexpr int CSR_EL = 16;            // elements per lane: leaves hold <= 128 = 8 x 16
+
+// v + (v of lane ^ 1, ^ 2, ^ 4): the 8-lane butterfly of a leaf's accumulators on DPP
+// (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror) -- no ds_bpermute address
+// registers held across the row loop.  Each step adds a commutative pair, so every lane of
+// the 8 holds the same ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)) bits as the shuffle version.
+template <int CTRL>
+__device__ __forceinline__ double csr_dpp(double v) {
+  const int2 u = __builtin_bit_cast(int2, v);
+  int2 r;
+  r.x = __builtin_amdgcn_update_dpp(0, u.x, CTRL, 0xf, 0xf, false);
+  r.y = __builtin_amdgcn_update_dpp(0, u.y, CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double csr_leaf_sum8(double r) {
+  r = r + csr_dpp<0xB1>(r);     // quad_perm [1,0,3,2]: lane ^ 1
+  r = r + csr_dpp<0x4E>(r);     // quad_perm [2,3,0,1]: lane ^ 2
+  r = r + csr_dpp<0x141>(r);    // row_half_mirror: lane 7 - i, the other quad of the 8
+  return r;
+}
 template <int OP>
 __global__ void __launch_bounds__(CSR_NT, 8)
 k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
@@ -177,8 +196,6 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
   const int L = sv.L(), R = sv.R();
   const int leaf = tid >> 3, j = tid & 7;
   const bool act = leaf < L;
-  const int st = act ? sv.lstart(leaf) : 0, len = act ? sv.llen(leaf) : 0;
-  const int stop = len - (len & 7), nfull = stop >> 3;
   const int32_t* tr = sv.trip();
   // combine rounds of wave 0 (the schedule's tree), result in nodes[0]
   auto combine = [&]() {
@@ -192,6 +209,10 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
     }
   };
   for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+    // the leaf geometry is re-read from the LDS schedule per row (two LDS reads) rather
+    // than held across the row loop, where it would spill
+    const int st = act ? sv.lstart(leaf) : 0, len = act ? sv.llen(leaf) : 0;
+    const int stop = len - (len & 7), nfull = stop >> 3;
     const double* x = X + row * ld;
     double xv[CSR_EL];
 #pragma unroll
@@ -208,15 +229,19 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
         c += t == t;
       }
     }
-    r = r + __shfl_xor(r, 1);
-    r = r + __shfl_xor(r, 2);
-    r = r + __shfl_xor(r, 4);
+    r = csr_leaf_sum8(r);
     if (act && j == 0) {
       for (int q = stop; q < len; ++q) { const double t = x[st + q]; r += t == t ? t : 0.0; c += t == t; }
       nodes[leaf] = r;
     }
+    // the wave's valid count from the bit planes of the lanes' counts (c < 32): ballots +
+    // scalar popcounts, no cross-lane shuffles
+    {
+      int cw = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      for (int b = 0; b < 5; ++b) cw += __popcll(__ballot((c >> b) & 1)) << b;
+      c = cw;
+    }
     if (lane == 0) iscr[wid] = c;
     __syncthreads();
     combine();
@@ -241,9 +266,7 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
           q2 = i == 0 ? q : q2 + q;
         }
       }
-      q2 = q2 + __shfl_xor(q2, 1);
-      q2 = q2 + __shfl_xor(q2, 2);
-      q2 = q2 + __shfl_xor(q2, 4);
+      q2 = csr_leaf_sum8(q2);
       if (act && j == 0) {
         for (int q = stop; q < len; ++q) {
           const double t = x[st + q];
@@ -271,21 +294,24 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
         if (nts) __builtin_nontemporal_store(v, p);
         else *p = v;
       };
+      // market_neutralize of the same row from the same moments (sd in {0, NaN} -> 0),
+      // stored next to each z so no output value stays live across a second loop
+      const bool two = OP == FMX_CS_ZSCORE && Y2;
+      const bool g2 = sd == 0.0 || sd != sd;
+      double* y2 = two ? Y2 + row * ld : nullptr;
 #pragma unroll
       for (int i = 0; i < CSR_EL; ++i)
-        if (i < nfull) put(outv(xv[i]), y + st + j + 8 * i);
+        if (i < nfull) {
+          const double o = outv(xv[i]);
+          put(o, y + st + j + 8 * i);
+          if (two) put(g2 ? 0.0 : o, y2 + st + j + 8 * i);
+        }
       if (act && j == 0)
-        for (int q = stop; q < len; ++q) y[st + q] = outv(x[st + q]);
-      if (OP == FMX_CS_ZSCORE && Y2) {
-        // market_neutralize of the same row from the same moments (sd in {0, NaN} -> 0)
-        const bool g2 = sd == 0.0 || sd != sd;
-        double* y2 = Y2 + row * ld;
-#pragma unroll
-        for (int i = 0; i < CSR_EL; ++i)
-          if (i < nfull) put(g2 ? 0.0 : outv(xv[i]), y2 + st + j + 8 * i);
-        if (act && j == 0)
-          for (int q = stop; q < len; ++q) y2[st + q] = g2 ? 0.0 : outv(x[st + q]);
-      }
+        for (int q = stop; q < len; ++q) {
+          const double o = outv(x[st + q]);
+          y[st + q] = o;
+          if (two) y2[st + q] = g2 ? 0.0 : o;
+        }
     }
     __syncthreads();                                   // nodes / iscr reused by the next row
   }

@@ -531,14 +531,21 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   double xr[EPT];
   // next chunk to load (date index relative to d0, asset block), walked by counters
   int64_t ld_d = c0 / nch, ld_a = c0 - (c0 / nch) * nch;
+  // one 64-bit row address per issue, made opaque so the compiler cannot hoist the EPT
+  // per-element row offsets out of the chunk loop (they spilled, and every reload's
+  // vmcnt(0) wait serialised the chunk's loads); element u is SG_NT / 32 rows further on
   auto issue = [&]() {
     const int64_t d = d0 + ld_d, a0 = ld_a * SG_K;
     if (++ld_a == nch) { ld_a = 0; ++ld_d; }
+    const int r0 = tid >> 5, cl = tid & 31;
+    const int64_t a = a0 + cl;
+    const double* xb = X + ((int64_t)r0 * D + d) * ld + a;
+    asm volatile("" : "+v"(xb));
+    const int64_t step = (int64_t)(SG_NT / 32) * D * ld;
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
-      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
-      const int64_t a = a0 + cl;
-      xr[u] = (e < NEL && r < F && a < A) ? X[((int64_t)r * D + d) * ld + a] : qnan();
+      const int e = tid + SG_NT * u, r = r0 + (SG_NT / 32) * u;
+      xr[u] = (e < NEL && r < F && a < A) ? xb[u * step] : qnan();
     }
   };
   auto load_stats = [&](int64_t dr) {             // date d0 + dr into buffer dr & 1
