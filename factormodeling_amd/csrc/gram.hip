@@ -1231,7 +1231,12 @@ k_valid_bits(const double* __restrict__ X, const double* __restrict__ stats, int
 }
 
 // k_gram_f64 over the raw panel: the chunk's rows are z-scored as they are staged
-// (valid = sd > 0 and x not NaN: (x - mean) / sd, else 0 -- k_zscore_exposures' values).
+// (valid = sd > 0 and x not NaN: (x - mean) * (1 / sd), else 0), double-buffered LDS
+// (139 KB, one workgroup per CU, one barrier per chunk).  The reciprocal is taken once per
+// row and chunk: z within an ulp of the division, G within 1e-12 relative of the
+// materialised path.  Measured at C4 (profiles/r03): 8 divisions per staged row cost 86 ms
+// of the 908 ms Gram stage -- the staging VALU is not hidden behind the MFMAs; a
+// single-buffered variant (two workgroups per CU) needs > 128 VGPRs and spills.
 template <bool VEC>
 __global__ void __launch_bounds__(512)
 k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
@@ -1267,21 +1272,17 @@ k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_
   auto stage = [&](int buf) {
     double* As = gsm + buf * 2 * GT * GKP;
     double* Bs = As + GT * GKP;
+    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;
+    const double ia = 1.0 / sa.y, ib = 1.0 / sb.y;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const double va = ra[u], vb = rb[u];
-      As[lr * GKP + lc + u] = (sa.y > 0.0 && va == va) ? (va - sa.x) / sa.y : 0.0;
-      Bs[lr * GKP + lc + u] = (sb.y > 0.0 && vb == vb) ? (vb - sb.x) / sb.y : 0.0;
+      As[lr * GKP + lc + u] = (oka && va == va) ? (va - sa.x) * ia : 0.0;
+      Bs[lr * GKP + lc + u] = (okb && vb == vb) ? (vb - sb.x) * ib : 0.0;
     }
   };
-  if (total > 0) {
-    issue(0);
-    stage(0);
-  }
-  __syncthreads();
-  if (total > 1) issue(1);
-  for (int64_t c = 0; c < total; ++c) {
-    const double* As = gsm + (c & 1) * 2 * GT * GKP;
+  auto mfma_chunk = [&](int buf) {
+    const double* As = gsm + buf * 2 * GT * GKP;
     const double* Bs = As + GT * GKP;
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
@@ -1297,7 +1298,16 @@ k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_
         for (int n = 0; n < 2; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
     }
-    if (c + 1 < total) stage((int)((c + 1) & 1));
+  };
+  if (total > 0) {
+    issue(0);
+    stage(0);
+  }
+  __syncthreads();
+  if (total > 1) issue(1);
+  for (int64_t c = 0; c < total; ++c) {
+    mfma_chunk((int)(c & 1));
+    if (c + 1 < total) stage((int)((c + 1) & 1));   // that buffer was last read in chunk c-1
     __syncthreads();
     if (c + 2 < total) issue(c + 2);
   }
@@ -1388,10 +1398,32 @@ struct DirectPlan {
   int64_t bytes() const { return bits_bytes() + part_bytes() + cnt_bytes(); }
   int64_t F;
 };
+// date slices for the direct Gram: enough workgroups for several rounds over the CUs and a
+// count that fills the last round (136 upper tiles x 8 slices = 1088 workgroups left the
+// fifth round of a one-workgroup-per-CU launch a quarter full)
+static GramPlan direct_gram_plan(int64_t F, int64_t d0, int64_t d1, int slots) {
+  GramPlan p;
+  p.nb = (int)ceil_div(F, GT);
+  p.ntile = (int64_t)p.nb * (p.nb + 1) / 2;
+  const int64_t ndates = d1 - d0;
+  const int64_t s0 = std::max<int64_t>(1, std::min<int64_t>(ndates, ceil_div((int64_t)4 * slots, p.ntile)));
+  int64_t best = s0;
+  double best_eff = 0.0;
+  for (int64_t s = s0; s <= std::min<int64_t>(ndates, 4 * s0); ++s) {
+    const int64_t wg = p.ntile * ceil_div(ndates, ceil_div(ndates, s));
+    const double eff = (double)wg / (double)(ceil_div(wg, (int64_t)slots) * slots);
+    if (eff > best_eff + 0.01) { best_eff = eff; best = s; }
+  }
+  p.dps = ceil_div(ndates, best);
+  p.nslice = ceil_div(ndates, p.dps);
+  return p;
+}
+
 static DirectPlan direct_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
   DirectPlan p;
   p.F = F;
-  p.g = gram_plan(F, A, d0, d1, false);
+  (void)A;
+  p.g = direct_gram_plan(F, d0, d1, 256);       // one k_gram_f64x workgroup per CU
   p.nd = d1 - d0;
   p.nwd = ceil_div(A, (int64_t)32);
   p.nw = p.nd * p.nwd;
@@ -1423,12 +1455,13 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   FMX_LAUNCH_CHECK("k_valid_bits");
   dim3 grid((unsigned)pl.g.ntile, (unsigned)pl.g.nslice);
   const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64x<true> : (const void*)k_gram_f64x<false>;
-  FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAM_F64_LDS));
+  const size_t lds = GRAM_F64_LDS;
+  FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int nb = pl.g.nb;
   int64_t dps = pl.g.dps, ntile = pl.g.ntile;
   void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
                   (void*)&dps, (void*)&nb, (void*)&ntile, (void*)&part};
-  FMX_HIP(hipLaunchKernel(k, grid, dim3(512), args, GRAM_F64_LDS, st));
+  FMX_HIP(hipLaunchKernel(k, grid, dim3(512), args, lds, st));
   k_gram_reduce<<<dim3((unsigned)pl.g.ntile, GT * GT / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, pl.g.nb, F,
                                                                           G, accumulate);
   FMX_LAUNCH_CHECK("k_gram_reduce");
