@@ -68,9 +68,11 @@ def bytes_per_unit(stage, F, ranked=False):
     return None
 
 
-# stage -> kernel-name prefix in the rocprofv3 PMC summary (profiles/traffic_c2.json)
+# stage -> kernel-name prefix in the rocprofv3 PMC summaries (profiles/traffic_c*.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
-                "ts_set": "fmx::k_ts_set<", "rank2": "fmx::k_cs_rank_fa<", "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
+                "ts_set": "fmx::k_ts_set<", "rank2": ("fmx::k_cs_rank_fa<1024, 10, false, false", "fmx::k_cs_rank_fa<"),
+                "ret:corr": "fmx::k_ts_corr_rl<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": "fmx::k_gram_f64x<",
+                "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
                 "rank_ic": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
@@ -78,23 +80,34 @@ STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic
                 "cs:market_neutralize": "fmx::k_cs_moment<2>", "ts:mean": "fmx::k_ts_reg<1,",
                 "ts:std": "fmx::k_ts_reg<2,", "ts:zscore": "fmx::k_ts_reg<4,", "ts:rank": "fmx::k_ts_reg<5,",
                 "ts:decay": "fmx::k_ts_reg<6,"}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_c2.json")
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f"traffic_{w}.json") for w in ("c2", "c4", "c5")]
 
 
 def pmc_traffic(stage, dims):
-    """HBM bytes per launch of the stage's kernel from the committed PMC summary (same
-    panel dims only), else None."""
-    try:
-        t = json.load(open(TRAFFIC_FILE))
-    except (OSError, ValueError):
-        return None
-    if list(t.get("dims", [])) != list(dims):
-        return None
+    """HBM bytes per launch of the stage's kernel from the committed PMC summaries
+    (tools/gpu_prof_r03.sh + tools/pmc_traffic.py): the summary of the same panel dims, or
+    one of the same assets x factors on fewer dates (C4 / C5 are captured on 252 of the
+    2520 dates: per-unit bytes x this launch's units), else None."""
     parts = stage.split(":")
     pre = STAGE_KERNEL.get(":".join(parts[:2]).rstrip(":")) or STAGE_KERNEL.get(parts[0])
-    for name, v in t.get("kernels", {}).items():
-        if pre and name.startswith(pre if isinstance(pre, tuple) else (pre,)):
-            return v["traffic_bytes"]
+    if not pre:
+        return None
+    pres = pre if isinstance(pre, tuple) else (pre,)
+    for path in TRAFFIC_FILES:
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        td = list(t.get("dims", []))
+        if td[1:] != list(dims)[1:]:
+            continue
+        ks = t.get("kernels", {})
+        for p in pres:                       # the first prefix with a match wins
+            for name in sorted(ks):
+                if name.startswith(p):
+                    v = ks[name]
+                    return v["traffic_bytes"] if td == list(dims) else v["traffic_per_unit"] * float(
+                        dims[0]) * dims[1] * dims[2]
     return None
 
 
@@ -334,8 +347,9 @@ def main():
         # G = Z^T Z, D*A*F*(F+1) flop (SURVEY 8(d) quotes the full square, 2*D*A*F^2)
         flops = float(sp.X.shape[1] - sp.halo) * A * F * (F + 1)
         tf = flops / (gram_ms * 1e-3) / 1e12
+        gtraffic = pmc_traffic("gram", [sp.X.shape[1], A, F]) if world == 1 else None
         roofline = {"kernel": "gram", "bound": "mfma", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": tf / FP64_PEAK_TFS, "traffic": None, "algorithmic_flops": flops, "ms": gram_ms}
+                    "frac": tf / FP64_PEAK_TFS, "traffic": gtraffic, "algorithmic_flops": flops, "ms": gram_ms}
     if args.stages and rank == 0:
         for k, v in sorted(stages.items(), key=lambda kv: -kv[1]):
             print(f"stage {k:28s} {v / args.steps:9.3f} ms", file=sys.stderr)

@@ -1211,6 +1211,8 @@ extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, do
 // (2) k_gram_f64x: k_gram_f64 with the z-score applied while a chunk is staged (X + the
 // row's (mean, sd) instead of Z); (3) k_gram_popc_fm: N = M M^T as AND + popcount of the
 // bits (exact integers), 64 x 64 tiles, 4 x 4 pairs per thread.
+namespace fmx {
+
 __global__ void __launch_bounds__(256)
 k_valid_bits(const double* __restrict__ X, const double* __restrict__ stats, int64_t D, int64_t A, int64_t ld,
              int64_t d0, int64_t nd, int64_t nwd, uint32_t* __restrict__ bits) {
@@ -1388,6 +1390,8 @@ __global__ void k_gram_counts(const unsigned long long* __restrict__ ncnt, int64
   N[i * F + j] = n;
   N[j * F + i] = n;
 }
+
+}  // namespace fmx
 
 struct DirectPlan {
   GramPlan g;

@@ -92,7 +92,15 @@ OPS = {
     "cs_rw_ic": (lambda X, R, Y: E.cs_rank_winsor_ic(X, R, (1, 2), 0.01, 0.99, Y, _set_outs(X)["mean"],
                                                      rank2=_RK.setdefault("rk", torch.empty(X.shape, dtype=E.RANK2_DTYPE,
                                                                                             device=X.device))), 24),
+    "ts_corr60": (lambda X, R, Y: E.ts_corr(X, R, 60, out=Y), 16),
+    "cvf60": (lambda X, R, Y: E.corr_vol_feature(X, Y, 60, out=_set_outs(X)["mean"]), 24),
+    "rank2": (lambda X, R, Y: E.cs_rank2(X, _RK.setdefault("rk2", torch.empty(X.shape, dtype=E.RANK2_DTYPE,
+                                                                              device=X.device))), 10),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
+    # the C2 step's Gram: exact fixed-point partials from the cs_zscore output (Y after cs_zn)
+    "gram_exact_z": (lambda X, R, Y: E.gram_exact(Y, None), 8),
+    # the C4 step's Gram straight from the panel (row stats + validity bits + tiles + popcount)
+    "gram_direct": (lambda X, R, Y: E.gram_direct(X), 8),
     "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
     "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
 }
