@@ -1326,6 +1326,173 @@ k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_
       }
 }
 
+// Wide tiles for the direct Gram: 256 (i) x 128 (j) per workgroup, 16 waves as 4 x 4, each a
+// 64 x 32 sub-tile of 4 x 2 fp64 16x16x4 MFMAs; K chunks of 16 assets, double-buffered LDS
+// (2 x 384 x 18 doubles = 110 KB: one workgroup and four waves per SIMD per CU).  Against
+// k_gram_f64x's 128 x 128 tiles: twice the waves to cover LDS and load latency, and the
+// i-panels are re-read by half as many tiles.  Tile (bi, bj) covers rows [256 bi, +256),
+// columns [128 bj, +128) for bj >= 2 bi: every (i <= j) pair lies in exactly one tile.
+constexpr int GW_I = 256, GW_J = 128, GW_K = 16, GW_KP = GW_K + 2;   // row pitch 36 dwords: conflict-free b64
+constexpr size_t GRAM_W_LDS = sizeof(double) * 2 * (GW_I + GW_J) * GW_KP;
+__host__ __device__ inline int64_t gw_ntile(int64_t F) {
+  const int64_t nbi = (F + GW_I - 1) / GW_I, nbj = (F + GW_J - 1) / GW_J;
+  int64_t n = 0;
+  for (int64_t bi = 0; bi < nbi; ++bi) n += nbj - 2 * bi > 0 ? nbj - 2 * bi : 0;
+  return n;
+}
+__device__ __forceinline__ void gw_tile(int t, int64_t F, int& bi, int& bj) {
+  const int nbj = (int)((F + GW_J - 1) / GW_J);
+  bi = 0;
+  while (t >= nbj - 2 * bi) { t -= nbj - 2 * bi; ++bi; }
+  bj = 2 * bi + t;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(1024)
+k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
+            int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t ntile, int64_t nslice, int xcd,
+            double* __restrict__ part) {
+  extern __shared__ double gsm[];             // [2][As (256 x KP) | Bs (128 x KP)]
+  constexpr int BUF = (GW_I + GW_J) * GW_KP;
+  // work item = slice * ntile + tile.  xcd: workgroups are dealt round-robin to the 8 XCDs,
+  // so XCD x's k-th workgroup takes item x * per + k -- each XCD walks a contiguous run of
+  // items (one date range, neighbouring tiles sharing row panels) and its L2 serves the
+  // shared panels; else item = workgroup id.
+  const int64_t total = ntile * nslice, wg = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  int64_t item = wg;
+  if (xcd == 1) {
+    const int64_t per = (total + 7) / 8;
+    item = (wg % 8) * per + wg / 8;
+  }
+  if (item >= total) return;                  // whole workgroup: before any barrier
+  const int64_t tile = item % ntile, slice = item / ntile;
+  int bi, bj;
+  gw_tile((int)tile, F, bi, bj);
+  const int i0 = bi * GW_I, j0 = bj * GW_J;
+  const int64_t ds = d0 + slice * dates_per_slice;
+  const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  dbl4 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
+  // loaders: A row tid >> 2 (4 assets at (tid & 3) * 4), B row tid >> 3 (2 assets at (tid & 7) * 2)
+  const int ar = tid >> 2, ac = (tid & 3) * 4, br = tid >> 3, bc = (tid & 7) * 2;
+  // 16 x 16 blocks this wave must compute (wave-uniform): not wholly below the diagonal
+  // (i > j everywhere: never read) and not wholly past F -- a tile straddling the diagonal
+  // skips the MFMAs of its lower half
+  uint32_t live = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int gi = i0 + wr * 64 + m * 16, gj = j0 + wc * 32 + n * 16;
+      if (gi <= gj + 15 && gi < F && gj < F) live |= 1u << (m * 2 + n);
+    }
+  const bool rowA = (i0 + ar) < F, rowB = (j0 + br) < F;
+  const int64_t nch = (A + GW_K - 1) / GW_K;
+  const int64_t nchunk = (de - ds) * nch;
+  double ra[4], rb[2];
+  double2 sa, sb;                             // (mean, sd) of the staged rows' date
+  auto issue = [&](int64_t c) {
+    const int64_t d = ds + c / nch, a0 = (c % nch) * GW_K;
+    const double* pa = X + ((int64_t)(i0 + ar) * D + d) * ld + a0 + ac;
+    const double* pb = X + ((int64_t)(j0 + br) * D + d) * ld + a0 + bc;
+    if (VEC && rowA && a0 + ac + 4 <= A) {
+      const dbl2 u = reinterpret_cast<const dbl2*>(pa)[0], v = reinterpret_cast<const dbl2*>(pa)[1];
+      ra[0] = u[0]; ra[1] = u[1]; ra[2] = v[0]; ra[3] = v[1];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ra[q] = (rowA && a0 + ac + q < A) ? pa[q] : qnan();
+    }
+    if (VEC && rowB && a0 + bc + 2 <= A) {
+      const dbl2 u = reinterpret_cast<const dbl2*>(pb)[0];
+      rb[0] = u[0]; rb[1] = u[1];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) rb[q] = (rowB && a0 + bc + q < A) ? pb[q] : qnan();
+    }
+    const double2* z = reinterpret_cast<const double2*>(zst);   // stats [F][D] (mean, sd)
+    sa = rowA ? z[(int64_t)(i0 + ar) * D + d] : make_double2(0.0, 0.0);
+    sb = rowB ? z[(int64_t)(j0 + br) * D + d] : make_double2(0.0, 0.0);
+  };
+  auto stage = [&](int buf) {
+    double* As = gsm + buf * BUF;
+    double* Bs = As + GW_I * GW_KP;
+    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;
+    const double ia = 1.0 / sa.y, ib = 1.0 / sb.y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = (oka && ra[q] == ra[q]) ? (ra[q] - sa.x) * ia : 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = (okb && rb[q] == rb[q]) ? (rb[q] - sb.x) * ib : 0.0;
+  };
+  auto mfma_chunk = [&](int buf) {
+    const double* As = gsm + buf * BUF;
+    const double* Bs = As + GW_I * GW_KP;
+#pragma unroll
+    for (int kk = 0; kk < GW_K; kk += 4) {
+      const int k = kk + (lane >> 4);
+      double af[4], bf[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) af[m] = As[(wr * 64 + m * 16 + (lane & 15)) * GW_KP + k];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) bf[n] = Bs[(wc * 32 + n * 16 + (lane & 15)) * GW_KP + k];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          if ((live >> (m * 2 + n)) & 1u)
+            acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+      // one k-step's fragments live at a time (the next step's reads are not hoisted over
+      // these MFMAs): 128 VGPRs at four waves per SIMD without spilling
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (nchunk > 0) {
+    issue(0);
+    stage(0);
+  }
+  __syncthreads();
+  if (nchunk > 1) issue(1);
+  for (int64_t c = 0; c < nchunk; ++c) {
+    mfma_chunk((int)(c & 1));
+    if (c + 1 < nchunk) stage((int)((c + 1) & 1));   // that buffer was last read in chunk c-1
+    __syncthreads();
+    if (c + 2 < nchunk) issue(c + 2);
+  }
+  double* p = part + (slice * ntile + tile) * (GW_I * GW_J);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;
+        const int col = wc * 32 + n * 16 + (lane & 15);
+        p[row * GW_J + col] = acc[m][n][r];
+      }
+}
+
+// G from k_gram_f64w's slice partials: the pairs i <= j of each tile, summed over the
+// slices in order (deterministic) and mirrored.
+__global__ void k_gram_reduce_w(const double* __restrict__ part, int64_t nslice, int64_t ntile, int64_t F,
+                                double* __restrict__ G, int accumulate) {
+  const int64_t tile = blockIdx.x;
+  int bi, bj;
+  gw_tile((int)tile, F, bi, bj);
+  const int e = blockIdx.y * blockDim.x + threadIdx.x;
+  if (e >= GW_I * GW_J) return;
+  const int64_t i = (int64_t)bi * GW_I + e / GW_J, j = (int64_t)bj * GW_J + e % GW_J;
+  if (i > j || j >= F) return;
+  double s = 0.0;
+  for (int64_t sl = 0; sl < nslice; ++sl) s += part[(sl * ntile + tile) * (GW_I * GW_J) + e];
+  if (accumulate) s += G[i * F + j];
+  G[i * F + j] = s;
+  G[j * F + i] = s;
+}
+
 // N[i][j] = sum over the bit words of popcount(bits[i] & bits[j]), factor-major bits
 // [F][nw]: one workgroup per (64 x 64 upper tile, word range); 64-word chunks of the tile's
 // 2 x 64 rows staged in LDS; thread (ty, tx) owns rows ty + 16 r and columns tx + 16 c
@@ -1394,10 +1561,10 @@ __global__ void k_gram_counts(const unsigned long long* __restrict__ ncnt, int64
 }  // namespace fmx
 
 struct DirectPlan {
-  GramPlan g;
+  GramPlan g;                                   // g.ntile: k_gram_f64w tiles (256 x 128)
   int64_t nd, nwd, nw;
   int64_t bits_bytes() const { return SmallPlan::align256((int64_t)sizeof(uint32_t) * F * nw); }
-  int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * g.part_elems()); }
+  int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * g.nslice * g.ntile * GW_I * GW_J); }
   int64_t cnt_bytes() const { return (int64_t)sizeof(unsigned long long) * F * F; }
   int64_t bytes() const { return bits_bytes() + part_bytes() + cnt_bytes(); }
   int64_t F;
@@ -1407,8 +1574,8 @@ struct DirectPlan {
 // fifth round of a one-workgroup-per-CU launch a quarter full)
 static GramPlan direct_gram_plan(int64_t F, int64_t d0, int64_t d1, int slots) {
   GramPlan p;
-  p.nb = (int)ceil_div(F, GT);
-  p.ntile = (int64_t)p.nb * (p.nb + 1) / 2;
+  p.nb = 0;
+  p.ntile = gw_ntile(F);
   const int64_t ndates = d1 - d0;
   const int64_t s0 = std::max<int64_t>(1, std::min<int64_t>(ndates, ceil_div((int64_t)4 * slots, p.ntile)));
   int64_t best = s0;
@@ -1457,18 +1624,20 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
   k_valid_bits<<<dim3((unsigned)pl.nd, (unsigned)F), 256, 0, st>>>(X, stats, D, A, ld, d0, pl.nd, pl.nwd, bits);
   FMX_LAUNCH_CHECK("k_valid_bits");
-  dim3 grid((unsigned)pl.g.ntile, (unsigned)pl.g.nslice);
-  const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64x<true> : (const void*)k_gram_f64x<false>;
-  const size_t lds = GRAM_F64_LDS;
+  const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64w<true> : (const void*)k_gram_f64w<false>;
+  const size_t lds = GRAM_W_LDS;
   FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int nb = pl.g.nb;
-  int64_t dps = pl.g.dps, ntile = pl.g.ntile;
+  int64_t dps = pl.g.dps, ntile = pl.g.ntile, nslice = pl.g.nslice;
+  static const int xcd = [] { const char* e = getenv("FMX_GRAM_XCD"); return e ? atoi(e) : 1; }();
+  int xcd_arg = xcd;
+  const int64_t nwg = xcd == 1 ? 8 * ((ntile * nslice + 7) / 8) : ntile * nslice;
   void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
-                  (void*)&dps, (void*)&nb, (void*)&ntile, (void*)&part};
-  FMX_HIP(hipLaunchKernel(k, grid, dim3(512), args, lds, st));
-  k_gram_reduce<<<dim3((unsigned)pl.g.ntile, GT * GT / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, pl.g.nb, F,
-                                                                          G, accumulate);
-  FMX_LAUNCH_CHECK("k_gram_reduce");
+                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&part};
+  const dim3 grid = xcd == 2 ? dim3((unsigned)ntile, (unsigned)nslice) : dim3((unsigned)nwg);
+  FMX_HIP(hipLaunchKernel(k, grid, dim3(1024), args, lds, st));
+  k_gram_reduce_w<<<dim3((unsigned)pl.g.ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, F,
+                                                                                 G, accumulate);
+  FMX_LAUNCH_CHECK("k_gram_reduce_w");
   FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
   const int T = (int)ceil_div(F, (int64_t)PF_T);
   const int ntp = T * (T + 1) / 2;
