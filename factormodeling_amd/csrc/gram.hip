@@ -1208,7 +1208,7 @@ extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, do
 // materialisation.  The row moments are the caller's fmx_cs_moment_stats (numpy pairwise
 // mean / std ddof=0: the oracle's z-score spec bit-for-bit, as the F <= 256 Gram uses).
 // (1) k_valid_bits: validity bits (x not NaN, sigma > 0), factor-major [F][nd][nwd];
-// (2) k_gram_f64x: k_gram_f64 with the z-score applied while a chunk is staged (X + the
+// (2) k_gram_f64w: G on fp64 MFMA with the z-score applied while a chunk is staged (X + the
 // row's (mean, sd) instead of Z); (3) k_gram_popc_fm: N = M M^T as AND + popcount of the
 // bits (exact integers), 64 x 64 tiles, 4 x 4 pairs per thread.
 namespace fmx {
@@ -1232,105 +1232,15 @@ k_valid_bits(const double* __restrict__ X, const double* __restrict__ stats, int
   }
 }
 
-// k_gram_f64 over the raw panel: the chunk's rows are z-scored as they are staged
-// (valid = sd > 0 and x not NaN: (x - mean) * (1 / sd), else 0), double-buffered LDS
-// (139 KB, one workgroup per CU, one barrier per chunk).  The reciprocal is taken once per
-// row and chunk: z within an ulp of the division, G within 1e-12 relative of the
-// materialised path.  Measured at C4 (profiles/r03): 8 divisions per staged row cost 86 ms
-// of the 908 ms Gram stage -- the staging VALU is not hidden behind the MFMAs; a
-// single-buffered variant (two workgroups per CU) needs > 128 VGPRs and spills.
-template <bool VEC>
-__global__ void __launch_bounds__(512)
-k_gram_f64x(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
-            int64_t d0, int64_t d1, int64_t dates_per_slice, int nb, int64_t ntile, double* __restrict__ part) {
-  extern __shared__ double gsm[];             // [2][As | Bs], GT * GKP doubles each
-  const int64_t tile = blockIdx.x, slice = blockIdx.y;
-  int ti, tj;
-  upper_tile((int)tile, nb, ti, tj);
-  const int i0 = ti * GT, j0 = tj * GT;
-  const int64_t ds = d0 + slice * dates_per_slice;
-  const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  dbl4 acc[4][2];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
-  const int lr = tid >> 2, lc = (tid & 3) * 8;
-  const bool rowA = (i0 + lr) < F, rowB = (j0 + lr) < F;
-  const int64_t nch = (A + GK - 1) / GK;
-  const int64_t total = (de - ds) * nch;
-  double ra[8], rb[8];
-  double2 sa, sb;                             // (mean, sd) of the staged rows' date
-  auto issue = [&](int64_t c) {
-    const int64_t d = ds + c / nch, a0 = (c % nch) * GK;
-    load_chunk<VEC, true>(X + ((int64_t)(i0 + lr) * D + d) * ld, rowA, a0, lc, A, ra);
-    load_chunk<VEC, true>(X + ((int64_t)(j0 + lr) * D + d) * ld, rowB, a0, lc, A, rb);
-    const double2* z = reinterpret_cast<const double2*>(zst);   // stats [F][D] (mean, sd)
-    sa = rowA ? z[(int64_t)(i0 + lr) * D + d] : make_double2(0.0, 0.0);
-    sb = rowB ? z[(int64_t)(j0 + lr) * D + d] : make_double2(0.0, 0.0);
-  };
-  auto stage = [&](int buf) {
-    double* As = gsm + buf * 2 * GT * GKP;
-    double* Bs = As + GT * GKP;
-    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;
-    const double ia = 1.0 / sa.y, ib = 1.0 / sb.y;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double va = ra[u], vb = rb[u];
-      As[lr * GKP + lc + u] = (oka && va == va) ? (va - sa.x) * ia : 0.0;
-      Bs[lr * GKP + lc + u] = (okb && vb == vb) ? (vb - sb.x) * ib : 0.0;
-    }
-  };
-  auto mfma_chunk = [&](int buf) {
-    const double* As = gsm + buf * 2 * GT * GKP;
-    const double* Bs = As + GT * GKP;
-#pragma unroll
-    for (int kk = 0; kk < GK; kk += 4) {
-      const int k = kk + (lane >> 4);
-      double af[4], bf[2];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = As[(wr * 64 + m * 16 + (lane & 15)) * GKP + k];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) bf[n] = Bs[(wc * 32 + n * 16 + (lane & 15)) * GKP + k];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
-    }
-  };
-  if (total > 0) {
-    issue(0);
-    stage(0);
-  }
-  __syncthreads();
-  if (total > 1) issue(1);
-  for (int64_t c = 0; c < total; ++c) {
-    mfma_chunk((int)(c & 1));
-    if (c + 1 < total) stage((int)((c + 1) & 1));   // that buffer was last read in chunk c-1
-    __syncthreads();
-    if (c + 2 < total) issue(c + 2);
-  }
-  double* p = part + (slice * ntile + tile) * (GT * GT);
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;
-        const int col = wc * 32 + n * 16 + (lane & 15);
-        p[row * GT + col] = acc[m][n][r];
-      }
-}
-
 // Wide tiles for the direct Gram: 256 (i) x 128 (j) per workgroup, 16 waves as 4 x 4, each a
 // 64 x 32 sub-tile of 4 x 2 fp64 16x16x4 MFMAs; K chunks of 16 assets, double-buffered LDS
-// (2 x 384 x 18 doubles = 110 KB: one workgroup and four waves per SIMD per CU).  Against
-// k_gram_f64x's 128 x 128 tiles: twice the waves to cover LDS and load latency, and the
-// i-panels are re-read by half as many tiles.  Tile (bi, bj) covers rows [256 bi, +256),
+// (2 x 384 x 18 doubles = 110 KB: one workgroup and four waves per SIMD per CU).  The
+// z-score is applied while a chunk is staged, (x - mean) * (1 / sd) with the reciprocal once
+// per row and chunk (dividing cost 86 ms of C4's Gram).  Measured against 128 x 128 tiles
+// of 8 waves (profiles/r03/c4_gram_direct_ab.log): half the HBM fetch (65 vs 136 GB per
+// launch at 252 dates) at the same time on one box -- the kernel is bound by the per-chunk
+// load -> stage -> barrier chain, not by MFMA (skipping the below-diagonal blocks' MFMAs
+// changed nothing) nor by HBM bandwidth.  Tile (bi, bj) covers rows [256 bi, +256),
 // columns [128 bj, +128) for bj >= 2 bi: every (i <= j) pair lies in exactly one tile.
 constexpr int GW_I = 256, GW_J = 128, GW_K = 16, GW_KP = GW_K + 2;   // row pitch 36 dwords: conflict-free b64
 constexpr size_t GRAM_W_LDS = sizeof(double) * 2 * (GW_I + GW_J) * GW_KP;
@@ -1594,7 +1504,7 @@ static DirectPlan direct_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
   DirectPlan p;
   p.F = F;
   (void)A;
-  p.g = direct_gram_plan(F, d0, d1, 256);       // one k_gram_f64x workgroup per CU
+  p.g = direct_gram_plan(F, d0, d1, 256);       // one k_gram_f64w workgroup per CU
   p.nd = d1 - d0;
   p.nwd = ceil_div(A, (int64_t)32);
   p.nw = p.nd * p.nwd;
