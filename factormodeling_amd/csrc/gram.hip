@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void gw_tile(int t, int64_t F, int& bi, int& bj) {
 template <bool VEC>
 __global__ void __launch_bounds__(1024)
 k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
-            int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t ntile, int64_t nslice, int xcd,
+            int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t ntile, int64_t nslice, int xcd, int opt,
             double* __restrict__ part) {
   extern __shared__ double gsm[];             // [2][As (256 x KP) | Bs (128 x KP)]
   constexpr int BUF = (GW_I + GW_J) * GW_KP;
@@ -1324,19 +1324,18 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
 #pragma unroll
       for (int q = 0; q < 2; ++q) rb[q] = (rowB && a0 + bc + q < A) ? pb[q] : qnan();
     }
-    const double2* z = reinterpret_cast<const double2*>(zst);   // stats [F][D] (mean, sd)
+    const double2* z = reinterpret_cast<const double2*>(zst);   // [F][D] (mean, 1/sd or 0)
     sa = rowA ? z[(int64_t)(i0 + ar) * D + d] : make_double2(0.0, 0.0);
     sb = rowB ? z[(int64_t)(j0 + br) * D + d] : make_double2(0.0, 0.0);
   };
   auto stage = [&](int buf) {
     double* As = gsm + buf * BUF;
     double* Bs = As + GW_I * GW_KP;
-    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;
-    const double ia = 1.0 / sa.y, ib = 1.0 / sb.y;
+    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;           // 1/sd > 0 <=> sd > 0
 #pragma unroll
-    for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = (oka && ra[q] == ra[q]) ? (ra[q] - sa.x) * ia : 0.0;
+    for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = (oka && ra[q] == ra[q]) ? (ra[q] - sa.x) * sa.y : 0.0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = (okb && rb[q] == rb[q]) ? (rb[q] - sb.x) * ib : 0.0;
+    for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = (okb && rb[q] == rb[q]) ? (rb[q] - sb.x) * sb.y : 0.0;
   };
   auto mfma_chunk = [&](int buf) {
     const double* As = gsm + buf * BUF;
@@ -1366,11 +1365,21 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   }
   __syncthreads();
   if (nchunk > 1) issue(1);
+  // half the waves of each SIMD (waves s, s+4, s+8, s+12 share SIMD s) stage chunk c+1 and
+  // issue chunk c+2's loads before their MFMAs of chunk c, half after: the SIMD's MFMA pipe
+  // is fed while the other half does its staging VALU work and waits on its loads
+  const bool stage_first = (opt & 1) && ((wid >> 2) & 1);
   for (int64_t c = 0; c < nchunk; ++c) {
+    auto next = [&]() {
+      if (c + 1 < nchunk) {
+        stage((int)((c + 1) & 1));            // that buffer was last read in chunk c-1
+        if (c + 2 < nchunk) issue(c + 2);
+      }
+    };
+    if (stage_first) next();
     mfma_chunk((int)(c & 1));
-    if (c + 1 < nchunk) stage((int)((c + 1) & 1));   // that buffer was last read in chunk c-1
+    if (!stage_first) next();
     __syncthreads();
-    if (c + 2 < nchunk) issue(c + 2);
   }
   double* p = part + (slice * ntile + tile) * (GW_I * GW_J);
 #pragma unroll
@@ -1383,6 +1392,15 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
         const int col = wc * 32 + n * 16 + (lane & 15);
         p[row * GW_J + col] = acc[m][n][r];
       }
+}
+
+// (mean, sd) -> (mean, 1/sd), 0 for sigma in {0, NaN}: the tile kernel's staging multiplies
+__global__ void k_inv_stats(const double* __restrict__ stats, double* __restrict__ zi, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double m = stats[2 * e], sd = stats[2 * e + 1];
+  zi[2 * e] = m;
+  zi[2 * e + 1] = sd > 0.0 ? 1.0 / sd : 0.0;
 }
 
 // G from k_gram_f64w's slice partials: the pairs i <= j of each tile, summed over the
@@ -1476,8 +1494,9 @@ struct DirectPlan {
   int64_t bits_bytes() const { return SmallPlan::align256((int64_t)sizeof(uint32_t) * F * nw); }
   int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * g.nslice * g.ntile * GW_I * GW_J); }
   int64_t cnt_bytes() const { return (int64_t)sizeof(unsigned long long) * F * F; }
-  int64_t bytes() const { return bits_bytes() + part_bytes() + cnt_bytes(); }
-  int64_t F;
+  int64_t inv_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * 2 * F * D); }
+  int64_t bytes() const { return bits_bytes() + part_bytes() + SmallPlan::align256(cnt_bytes()) + inv_bytes(); }
+  int64_t F, D;
 };
 // date slices for the direct Gram: enough workgroups for several rounds over the CUs and a
 // count that fills the last round (136 upper tiles x 8 slices = 1088 workgroups left the
@@ -1500,9 +1519,10 @@ static GramPlan direct_gram_plan(int64_t F, int64_t d0, int64_t d1, int slots) {
   return p;
 }
 
-static DirectPlan direct_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
+static DirectPlan direct_plan(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
   DirectPlan p;
   p.F = F;
+  p.D = D;
   (void)A;
   p.g = direct_gram_plan(F, d0, d1, 256);       // one k_gram_f64w workgroup per CU
   p.nd = d1 - d0;
@@ -1512,9 +1532,8 @@ static DirectPlan direct_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
 }
 
 extern "C" int64_t fmx_gram_direct_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
-  (void)D;
   if (F <= 0 || d1 <= d0) return 0;
-  return direct_plan(F, A, d0, d1).bytes();
+  return direct_plan(F, D, A, d0, d1).bytes();
 }
 
 extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, double* G, double* N, int64_t F,
@@ -1524,7 +1543,7 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1, "bad dims");
   FMX_ARG(F <= 65535 && d1 - d0 <= 0x7fffffff, "too many factors / dates");
   if (F == 0 || d1 == d0) return FMX_OK;
-  const DirectPlan pl = direct_plan(F, A, d0, d1);
+  const DirectPlan pl = direct_plan(F, D, A, d0, d1);
   if (fmx_status e = check_work(work, work_bytes, pl.bytes(), "fmx_gram_direct_work_bytes")) return e;
   hipStream_t st = as_stream(stream);
   char* w = static_cast<char*>(work);
@@ -1532,8 +1551,12 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   uint32_t* bits = reinterpret_cast<uint32_t*>(w);
   double* part = reinterpret_cast<double*>(w + pl.bits_bytes());
   unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
+  double* zinv = reinterpret_cast<double*>(w + pl.bits_bytes() + pl.part_bytes() + SmallPlan::align256(pl.cnt_bytes()));
   k_valid_bits<<<dim3((unsigned)pl.nd, (unsigned)F), 256, 0, st>>>(X, stats, D, A, ld, d0, pl.nd, pl.nwd, bits);
   FMX_LAUNCH_CHECK("k_valid_bits");
+  k_inv_stats<<<(unsigned)ceil_div(F * D, (int64_t)256), 256, 0, st>>>(stats, zinv, F * D);
+  FMX_LAUNCH_CHECK("k_inv_stats");
+  zst = zinv;
   const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64w<true> : (const void*)k_gram_f64w<false>;
   const size_t lds = GRAM_W_LDS;
   FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1541,8 +1564,10 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   static const int xcd = [] { const char* e = getenv("FMX_GRAM_XCD"); return e ? atoi(e) : 1; }();
   int xcd_arg = xcd;
   const int64_t nwg = xcd == 1 ? 8 * ((ntile * nslice + 7) / 8) : ntile * nslice;
+  static const int wopt = [] { const char* e = getenv("FMX_GRAM_WOPT"); return e ? atoi(e) : 1; }();
+  int wopt_arg = wopt;
   void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
-                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&part};
+                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg, (void*)&part};
   const dim3 grid = xcd == 2 ? dim3((unsigned)ntile, (unsigned)nslice) : dim3((unsigned)nwg);
   FMX_HIP(hipLaunchKernel(k, grid, dim3(1024), args, lds, st));
   k_gram_reduce_w<<<dim3((unsigned)pl.g.ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, F,
