@@ -3,7 +3,8 @@
 The selector functions keep the reference's plugin signature
 ``f(metrics_df, factors_win, returns_win, factor_ret_win, today, window, **kwargs) ->
 pd.Series`` (factor_selection_methods.py:6, :28, :119) so user code and the
-``FACTOR_SELECTION_METHODS`` registry keep working.  They are O(F) host functions; the
+``FACTOR_SELECTION_METHODS`` registry keep working.  icir_top and momentum are O(F) numpy
+functions; mvo (a cvxpy QP) is the reference's own selector, loaded by path.  The
 O(D x A x F) work they consume (window metrics) is computed on the GPU by
 ``factor_selector``, which also runs ``icir_top`` fully on the device when the registry
 entry is the built-in one.
@@ -19,28 +20,37 @@ import pandas as pd
 
 def icir_top_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window, icir_threshold=0.03,
                       top_x=5, use_rank_icir=True, **kwargs):
-    """factor_selection_methods.py:6-26"""
+    """Equal weights on the ``top_x`` factors whose (rank_)IC_IR exceeds ``icir_threshold``
+    (factor_selection_methods.py:6-26: ``nlargest`` over the thresholded frame, ties kept in
+    frame order -- a stable descending argsort here).  The pipeline's day-by-day selection
+    runs the same rule on the device (``k_select_icir_top``)."""
     col = "rank_IC_IR" if use_rank_icir else "IC_IR"
-    selected = metrics_df[metrics_df[col] > icir_threshold].nlargest(top_x, col)
-    vec = pd.Series(0.0, index=metrics_df.index, name=today)
-    vec.loc[selected.index] = 1.0
-    if vec.sum() > 0:
-        vec = vec / vec.sum()
-    return vec
+    v = metrics_df[col].to_numpy(dtype=np.float64)
+    with np.errstate(invalid="ignore"):
+        cand = np.flatnonzero(v > icir_threshold)              # NaN never passes
+    sel = cand[np.argsort(-v[cand], kind="stable")][:max(int(top_x), 0)]
+    w = np.zeros(len(v))
+    if sel.size:
+        w[sel] = 1.0 / sel.size
+    return pd.Series(w, index=metrics_df.index, name=today)
 
 
 def factor_momentum_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window, max_weight=1.0,
                              **kwargs):
-    """factor_selection_methods.py:28-58"""
-    factor_names = metrics_df.index.tolist()
-    momentum = factor_ret_win.loc[:, factor_names].sum()
-    momentum = momentum.clip(lower=0)
+    """Weights proportional to each factor's positive window return sum, optionally capped
+    at ``max_weight`` (factor_selection_methods.py:28-58).  The per-factor sums run over the
+    factor-major copy of the window (NaN -> 0), the same pairwise order as the reference's
+    column sums."""
+    names = metrics_df.index.tolist()
+    fw = np.ascontiguousarray(factor_ret_win.loc[:, names].to_numpy(dtype=np.float64, na_value=np.nan).T)
+    mom = np.where(np.isnan(fw), 0.0, fw).sum(axis=1)
+    mom = np.maximum(mom, 0.0)
     if max_weight < 1.0:
-        momentum = momentum.clip(upper=max_weight)
-    vec = pd.Series(0.0, index=momentum.index, name=today)
-    if momentum.sum() > 0:
-        vec = momentum / momentum.sum()
-    return vec
+        mom = np.minimum(mom, max_weight)
+    tot = mom.sum()
+    if tot > 0:                                  # (the reference's quotient Series is unnamed)
+        return pd.Series(mom / tot, index=pd.Index(names))
+    return pd.Series(np.zeros(len(names)), index=pd.Index(names), name=today)
 
 
 def ledoit_wolf_shrinkage(returns):
@@ -66,41 +76,32 @@ def ledoit_wolf_shrinkage(returns):
     return lam * target + (1 - lam) * sample_cov
 
 
+_REF_FSM = None
+
+
 def mvo_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window, risk_aversion=1.0,
                  max_weight=1.0, turnover_penalty=0.0, previous_weights=None, use_shrinkage=True, **kwargs):
-    """factor_selection_methods.py:119-175.  Host-side QP (out of the GPU scope); needs
-    cvxpy exactly like the reference."""
-    try:
-        import cvxpy as cp
-    except ImportError as e:  # pragma: no cover - cvxpy is absent in this image
-        raise ImportError("mvo_selector needs cvxpy (host QP solver), as in the reference") from e
-    factor_names = metrics_df.index.tolist()
-    n = len(factor_names)
-    mean = factor_ret_win[factor_names].mean()
-    if use_shrinkage:
-        cov = pd.DataFrame(ledoit_wolf_shrinkage(factor_ret_win[factor_names].values), index=factor_names,
-                           columns=factor_names)
-    else:
-        cov = factor_ret_win[factor_names].cov()
-    w = cp.Variable(n)
-    cov_matrix = 0.5 * (cov.values + cov.values.T)
-    obj = mean.values @ w - risk_aversion * cp.quad_form(w, cov_matrix)
-    if turnover_penalty > 0 and previous_weights is not None:
-        prev = previous_weights.reindex(factor_names).fillna(0).values
-        obj = obj - turnover_penalty * cp.norm1(w - prev)
-    constraints = [cp.sum(w) == 1, w >= 0, w <= (max_weight if max_weight < 1.0 else 1)]
-    prob = cp.Problem(cp.Maximize(obj), constraints)
-    try:
-        prob.solve()
-        weights = w.value
-        if weights is None:
-            weights = np.zeros(n)
-    except Exception:
-        weights = np.zeros(n)
-    vec = pd.Series(weights, index=factor_names, name=today)
-    if vec.sum() > 0:
-        vec = vec / vec.sum()
-    return vec
+    """Mean-variance factor weights (factor_selection_methods.py:119-175): a host cvxpy QP,
+    outside the GPU scope.  Handed to the reference's own selector, loaded by path from
+    ``$FMX_REFERENCE_DIR`` (as the drop-in ``Simulation`` does for its MVO methods), so the
+    solver setup is the reference's exactly; it needs cvxpy like the reference."""
+    global _REF_FSM
+    if _REF_FSM is None:
+        import importlib.util
+        import os
+        d = os.environ.get("FMX_REFERENCE_DIR")
+        path = os.path.join(d, "factor_selection_methods.py") if d else None
+        if not path or not os.path.exists(path):
+            raise NotImplementedError("mvo_selector runs the reference's host QP: set FMX_REFERENCE_DIR to the "
+                                      "FactorModeling checkout that holds factor_selection_methods.py")
+        spec = importlib.util.spec_from_file_location("_fmx_reference_factor_selection_methods", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _REF_FSM = mod
+    return _REF_FSM.mvo_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window,
+                                 risk_aversion=risk_aversion, max_weight=max_weight,
+                                 turnover_penalty=turnover_penalty, previous_weights=previous_weights,
+                                 use_shrinkage=use_shrinkage, **kwargs)
 
 
 def corr_prune_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window, rho=0.7, top_x=5,
