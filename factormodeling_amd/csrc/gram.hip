@@ -1207,7 +1207,8 @@ extern "C" fmx_status fmx_gram(const double* Z, const uint16_t* M, double* G, do
 // Wide-panel Gram straight from the panel (fmx_gram_direct, C4's 2000 x 2000): no Z / M
 // materialisation.  The row moments are the caller's fmx_cs_moment_stats (numpy pairwise
 // mean / std ddof=0: the oracle's z-score spec bit-for-bit, as the F <= 256 Gram uses).
-// (1) k_valid_bits: validity bits (x not NaN, sigma > 0), factor-major [F][nd][nwd];
+// (1) validity bits (x not NaN, sigma > 0), factor-major [F][nd][nwd], written by the
+// tile kernel's diagonal tiles while they stage (k_valid_bits: the standalone pass);
 // (2) k_gram_f64w: G on fp64 MFMA with the z-score applied while a chunk is staged (X + the
 // row's (mean, sd) instead of Z); (3) k_gram_popc_fm: N = M M^T as AND + popcount of the
 // bits (exact integers), 64 x 64 tiles, 4 x 4 pairs per thread.
@@ -1261,7 +1262,7 @@ template <bool VEC>
 __global__ void __launch_bounds__(1024)
 k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
             int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t ntile, int64_t nslice, int xcd, int opt,
-            double* __restrict__ part) {
+            double* __restrict__ part, uint16_t* __restrict__ bits16, int64_t nwd) {
   extern __shared__ double gsm[];             // [2][As (256 x KP) | Bs (128 x KP)]
   constexpr int BUF = (GW_I + GW_J) * GW_KP;
   // work item = slice * ntile + tile.  xcd: workgroups are dealt round-robin to the 8 XCDs,
@@ -1328,10 +1329,28 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
     sa = rowA ? z[(int64_t)(i0 + ar) * D + d] : make_double2(0.0, 0.0);
     sb = rowB ? z[(int64_t)(j0 + br) * D + d] : make_double2(0.0, 0.0);
   };
-  auto stage = [&](int buf) {
+  // validity bits: the diagonal tiles (bj = 2 bi, whose i-rows cover every row once per
+  // date) write them while staging -- half-word (16 assets) per row and chunk, in the
+  // factor-major [F][nd][2 nwd] u16 = [F][nd][nwd] u32 layout k_gram_popc_fm reads
+  const bool wbits = bits16 != nullptr && bj == 2 * bi;
+  auto stage = [&](int buf, int64_t c) {
     double* As = gsm + buf * BUF;
     double* Bs = As + GW_I * GW_KP;
     const bool oka = sa.y > 0.0, okb = sb.y > 0.0;           // 1/sd > 0 <=> sd > 0
+    if (wbits) {                                             // workgroup-uniform
+      // the row's 16 bits in (q, lane & 3) order: any asset order shared by every row
+      // gives the same AND / popcount pair counts
+      uint32_t hw = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t m = __ballot(rowA && oka && ra[q] == ra[q]);
+        hw |= (uint32_t)((m >> (lane & ~3)) & 0xfu) << (4 * q);
+      }
+      if ((lane & 3) == 0 && rowA) {
+        const int64_t dr = (ds - d0) + c / nch, j = c - (c / nch) * nch;
+        bits16[((int64_t)(i0 + ar) * (d1 - d0) + dr) * (2 * nwd) + j] = (uint16_t)hw;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = (oka && ra[q] == ra[q]) ? (ra[q] - sa.x) * sa.y : 0.0;
 #pragma unroll
@@ -1361,7 +1380,7 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   };
   if (nchunk > 0) {
     issue(0);
-    stage(0);
+    stage(0, 0);
   }
   __syncthreads();
   if (nchunk > 1) issue(1);
@@ -1372,7 +1391,7 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   for (int64_t c = 0; c < nchunk; ++c) {
     auto next = [&]() {
       if (c + 1 < nchunk) {
-        stage((int)((c + 1) & 1));            // that buffer was last read in chunk c-1
+        stage((int)((c + 1) & 1), c + 1);     // that buffer was last read in chunk c-1
         if (c + 2 < nchunk) issue(c + 2);
       }
     };
@@ -1552,8 +1571,9 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   double* part = reinterpret_cast<double*>(w + pl.bits_bytes());
   unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
   double* zinv = reinterpret_cast<double*>(w + pl.bits_bytes() + pl.part_bytes() + SmallPlan::align256(pl.cnt_bytes()));
-  k_valid_bits<<<dim3((unsigned)pl.nd, (unsigned)F), 256, 0, st>>>(X, stats, D, A, ld, d0, pl.nd, pl.nwd, bits);
-  FMX_LAUNCH_CHECK("k_valid_bits");
+  // the tile kernel writes the validity bits (its diagonal tiles); an odd chunk count per
+  // date leaves each date's last half-word unwritten: zero the bits first then
+  if (ceil_div(A, (int64_t)GW_K) % 2 == 1) FMX_HIP(hipMemsetAsync(bits, 0, pl.bits_bytes(), st));
   k_inv_stats<<<(unsigned)ceil_div(F * D, (int64_t)256), 256, 0, st>>>(stats, zinv, F * D);
   FMX_LAUNCH_CHECK("k_inv_stats");
   zst = zinv;
@@ -1564,10 +1584,13 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   static const int xcd = [] { const char* e = getenv("FMX_GRAM_XCD"); return e ? atoi(e) : 1; }();
   int xcd_arg = xcd;
   const int64_t nwg = xcd == 1 ? 8 * ((ntile * nslice + 7) / 8) : ntile * nslice;
+  uint16_t* bits16 = reinterpret_cast<uint16_t*>(bits);
+  int64_t nwd = pl.nwd;
   static const int wopt = [] { const char* e = getenv("FMX_GRAM_WOPT"); return e ? atoi(e) : 1; }();
   int wopt_arg = wopt;
   void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
-                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg, (void*)&part};
+                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg, (void*)&part,
+                  (void*)&bits16, (void*)&nwd};
   const dim3 grid = xcd == 2 ? dim3((unsigned)ntile, (unsigned)nslice) : dim3((unsigned)nwg);
   FMX_HIP(hipLaunchKernel(k, grid, dim3(1024), args, lds, st));
   k_gram_reduce_w<<<dim3((unsigned)pl.g.ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, F,
