@@ -8,10 +8,12 @@
 // column of the [F][D][ld] panel and walks its dates; at each date the 64 lanes of a
 // wave read 64 consecutive assets (coalesced 512-B rows).
 //
-// The window history is a thread-private ring in LDS laid out ring[slot*64 + lane]
-// (bank-conflict free, no barriers).  Rows whose presence byte is 0 are skipped: the
-// ring only advances on present rows, which reproduces the reference's row-based
-// windows on ragged panels.
+// No kernel keeps the window in LDS, so no window length is refused.  The moment and
+// shift ops only need the value LEAVING the window: a register ring for the hot windows
+// (k_ts_reg, k_ts_set), a re-read of x[d - W] on dense panels (k_ts_rl) or a trailing row
+// pointer on ragged ones (k_ts_ptr).  ts_rank / ts_decay need the whole window: k_ts_win
+// streams it per tile of dates.  Rows whose presence byte is 0 are not part of the
+// symbol's row sequence (the reference's row-based windows on ragged panels).
 //
 // The add/remove state machines replicate pandas 2.3.3 _libs/window/aggregations.pyx
 // (roll_sum / roll_mean / roll_var incl. Kahan compensation, the consecutive-same-
@@ -22,9 +24,6 @@
 #include "fmx_common.hpp"
 
 namespace fmx {
-
-constexpr int TS_BLOCK = 64;   // one wave per block: the LDS ring is thread-private
-constexpr int TS_UNROLL = 8;   // dates prefetched per lane
 
 struct SumSt {
   double s, ca, cr, prev;
@@ -132,77 +131,52 @@ struct VarSt {
 __device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v); }
 
 // ------------------------------------------------------------------------------------
-// Per-column walker state.  i counts the column's present rows; the column's window lives
-// in the LDS ring at ring[(slot * TS_BLOCK + lane) * V + u].
+// Per-column walker state.  i counts the column's present rows.
 struct ColState {
   SumSt ss;
   MeanSt ms;
   VarSt vs;
   double last;
   int64_t i;
-  int slot, nan_in_win;
+  int nan_in_win;
   bool first;
-  __device__ void init() { i = 0; slot = 0; nan_in_win = 0; first = true; last = qnan(); }
+  __device__ void init() { i = 0; nan_in_win = 0; first = true; last = qnan(); }
 };
 
-template <int OP, int V>
-__device__ __forceinline__ double ts_step(ColState& c, double v, int W, double* ring, int lane, int u) {
+// One rolling step of a moment / shift op given the value LEAVING the window (`old`, the
+// column's present row c.i - W; only read once c.i >= W).  Where that value comes from is
+// the caller's business: a register ring (k_ts_reg), a re-read of x[d - W] on dense panels
+// (k_ts_rl) or a trailing row pointer on ragged ones (k_ts_ptr) -- none of which bounds W.
+// OP in {SUM, MEAN, STD, VAR, ZSCORE, DIFF, DELAY, BACKFILL}.
+template <int OP>
+__device__ __forceinline__ double ts_moment(ColState& c, double v, double old, int W) {
   if (c.first) { c.ss.init(v); c.ms.init(v); c.vs.init(v); c.first = false; }
-  double old = qnan();
-  if (OP != FMX_TS_BACKFILL) {
-    double* rs = ring + ((int64_t)c.slot * TS_BLOCK + lane) * V + u;
-    if (c.i >= W) old = *rs;
-    *rs = v;
-    c.slot = (c.slot + 1 == W) ? 0 : c.slot + 1;
-  }
+  const bool full = c.i >= W;
   double out;
   if (OP == FMX_TS_SUM) {
-    if (c.i >= W) c.ss.remove(old);
+    if (full) c.ss.remove(old);
     c.ss.add(v);
     out = c.ss.result(W);
   } else if (OP == FMX_TS_MEAN) {
-    if (c.i >= W) c.ms.remove(old);
+    if (full) c.ms.remove(old);
     c.ms.add(v);
     out = c.ms.result(W);
   } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
-    if (c.i >= W) c.vs.remove(old);
+    if (full) c.vs.remove(old);
     c.vs.add(v);
     const double var = c.vs.var(W, 1);
     out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
   } else if (OP == FMX_TS_ZSCORE) {
-    if (c.i >= W) { c.ms.remove(old); c.vs.remove(old); }
+    if (full) { c.ms.remove(old); c.vs.remove(old); }
     c.ms.add(v); c.vs.add(v);
     const double m = c.ms.result(W);
     double sd = zsqrt(c.vs.var(W, 1));
     if (sd == 0.0) sd = qnan();
     out = (v - m) / sd;
-  } else if (OP == FMX_TS_RANK || OP == FMX_TS_DECAY) {
-    if (c.i >= W && old != old) c.nan_in_win -= 1;
-    if (v != v) c.nan_in_win += 1;
-    if (c.i + 1 < W || c.nan_in_win > 0) {
-      out = qnan();
-    } else if (OP == FMX_TS_RANK) {
-      int less = 0, eq = 0;
-      for (int k = 0; k < W; ++k) {
-        const double w = ring[((int64_t)k * TS_BLOCK + lane) * V + u];
-        less += (w < v);
-        eq += (w == v);
-      }
-      out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
-    } else {
-      // oldest element sits at `slot` (just advanced); weights 1..W oldest->newest
-      double acc = 0.0;
-      int sl = c.slot;
-      for (int k = 1; k <= W; ++k) {   // fused multiply-adds, as numpy's BLAS ddot
-        acc = __builtin_fma(ring[((int64_t)sl * TS_BLOCK + lane) * V + u], (double)k, acc);
-        sl = (sl + 1 == W) ? 0 : sl + 1;
-      }
-      out = acc / ((double)W * (double)(W + 1) / 2.0);
-    }
   } else if (OP == FMX_TS_DIFF) {
-    out = (c.i >= W) ? v - old : qnan();
+    out = full ? v - old : qnan();
   } else if (OP == FMX_TS_DELAY) {
-    out = (c.i >= W) ? old : qnan();
+    out = full ? old : qnan();
   } else {  // BACKFILL
     if (v == v) c.last = v;
     out = c.last;
@@ -449,7 +423,8 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
 // a dense panel is x[d - W] -- re-read from memory instead of kept in a ring (a 60-deep
 // LDS ring would hold one wave per 30 KB of LDS).  One lane per (factor, asset) column,
 // PF dates of both streams in flight; same state machines and operation order as
-// ts_step, so the outputs are bit-identical.  OP in {SUM, MEAN, STD, VAR, ZSCORE}.
+// ts_moment, so the outputs are bit-identical to every other path.
+// OP in {SUM, MEAN, STD, VAR, ZSCORE, DIFF, DELAY}.
 template <int OP, int PF>
 __global__ void __launch_bounds__(256)
 k_ts_rl(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld, int W) {
@@ -472,34 +447,212 @@ k_ts_rl(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t
     for (int q = 0; q < PF; ++q) {
       const int64_t d = d0 + q;
       if (d >= D) break;
-      const double vv = v[q];
-      if (c.first) { c.ss.init(vv); c.ms.init(vv); c.vs.init(vv); c.first = false; }
-      const bool full = c.i >= W;
-      double out;
-      if (OP == FMX_TS_SUM) {
-        if (full) c.ss.remove(o[q]);
-        c.ss.add(vv);
-        out = c.ss.result(W);
-      } else if (OP == FMX_TS_MEAN) {
-        if (full) c.ms.remove(o[q]);
-        c.ms.add(vv);
-        out = c.ms.result(W);
-      } else if (OP == FMX_TS_STD || OP == FMX_TS_VAR) {
-        if (full) c.vs.remove(o[q]);
-        c.vs.add(vv);
-        const double var = c.vs.var(W, 1);
-        out = (OP == FMX_TS_VAR) ? var : zsqrt(var);
-      } else {  // ZSCORE
-        if (full) { c.ms.remove(o[q]); c.vs.remove(o[q]); }
-        c.ms.add(vv); c.vs.add(vv);
-        const double m = c.ms.result(W);
-        double sd = zsqrt(c.vs.var(W, 1));
-        if (sd == 0.0) sd = qnan();
-        out = (vv - m) / sd;
-      }
-      y[d * ld] = out;
-      c.i += 1;
+      y[d * ld] = ts_moment<OP>(c, v[q], o[q], W);
     }
+  }
+}
+
+// Ragged panels (a presence byte per (date, asset); absent rows are not part of the
+// symbol's row sequence, operations.py's groupby('symbol') walk): the same column walk,
+// with the value leaving the window found by a TRAILING ROW POINTER -- the date of the
+// column's present row c.i - W, advanced past absent rows as the window slides.  The
+// pointer only moves forward, so a column costs O(D) whatever W is (no ring, no LDS, no
+// window cap).  The next leaving value is loaded as soon as the pointer moves, a step
+// ahead of its use.  Absent rows get NaN.  present == NULL means every row is present.
+// OP in {SUM, MEAN, STD, VAR, ZSCORE, DIFF, DELAY, BACKFILL}.
+template <int OP, int PF>
+__global__ void __launch_bounds__(256)
+k_ts_ptr(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld, int W,
+         const uint8_t* __restrict__ present) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  const uint8_t* pres = present ? present + a : nullptr;
+  ColState c;
+  c.init();
+  int64_t tail = -1;     // date of present row c.i - W (the next row to leave the window)
+  double oldv = 0.0;     // x at `tail`
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double v[PF];
+    bool p[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      v[q] = d < D ? x[d * ld] : 0.0;
+      p[q] = d < D && (pres == nullptr || pres[d * ld] != 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      if (!p[q]) { y[d * ld] = qnan(); continue; }
+      if (tail < 0) { tail = d; oldv = v[q]; }
+      double old = 0.0;
+      if (OP != FMX_TS_BACKFILL && c.i >= W) {
+        old = oldv;
+        // present row c.i - W + 1 is at or before d (row d is present): the walk stops there
+        do { ++tail; } while (pres != nullptr && pres[tail * ld] == 0);
+        oldv = x[tail * ld];
+      }
+      y[d * ld] = ts_moment<OP>(c, v[q], old, W);
+    }
+  }
+}
+
+// Negative windows of diff / delay (operations.py:34-38 with periods < 0: a LEAD of K
+// present rows, x.diff(-K) = x - x.shift(-K)).  Every row first gets NaN; when present
+// row i arrives, present row i - K (at the trailing pointer) is final.  Dense or ragged,
+// any K.
+template <int OP>
+__global__ void __launch_bounds__(256)
+k_ts_lead_ptr(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+              int K, const uint8_t* __restrict__ present) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const double* x = X + f * D * ld + a;
+  double* y = Y + f * D * ld + a;
+  const uint8_t* pres = present ? present + a : nullptr;
+  int64_t i = 0, tail = -1;
+  for (int64_t d = 0; d < D; ++d) {
+    y[d * ld] = qnan();
+    if (pres != nullptr && pres[d * ld] == 0) continue;
+    const double v = x[d * ld];
+    if (tail < 0) tail = d;
+    if (i >= K) {
+      const double ov = x[tail * ld];
+      y[tail * ld] = (OP == FMX_TS_DIFF) ? ov - v : v;   // same thread wrote its NaN earlier
+      do { ++tail; } while (pres != nullptr && pres[tail * ld] == 0);
+    }
+    ++i;
+  }
+}
+
+// ts_rank and ts_decay for ANY window, dense or ragged (operations.py:23-32, :40-48).
+// Both need the whole window at every row, so instead of a W-deep ring a thread owns a
+// TILE of T consecutive dates of one column and streams the W + T - 1 rows that feed them
+// once, oldest first, updating all T outputs per row from registers:
+//   decay:  acc_t = fma(x_p, k, acc_t) with weight k = p - q_t + W in 1..W (the same
+//           oldest->newest fma chain as the register-ring kernel: bit-identical to it);
+//   rank:   s_t += 2*(x_p < v_t) + (x_p == v_t), so #less + (#equal + 1)/2 = (s_t + 1)/2
+//           (the same half-integer, divided by W); a NaN in the window sets a flag bit.
+// p / q_t index the column's PRESENT rows (a ragged symbol's window is its last W rows):
+// the thread first walks back from its tile to the (W-1)th present row before it, then
+// forward; the lanes of a wave walk the same dates, so every row load is one coalesced
+// 512-B access.  Work O(W + T) per T outputs, registers O(T), LDS none -- no window cap.
+// Waves: 64 consecutive assets of one (factor, tile); 4 waves per block.
+constexpr int TSW_T = 16;
+constexpr int TSW_NANBIT = 0x40000000;
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int OP, int T>
+__global__ void __launch_bounds__(256)
+k_ts_win(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t D, int64_t A, int64_t ld, int W,
+         const uint8_t* __restrict__ present, int64_t achunks, int64_t ntiles) {
+  static_assert(T <= 30, "tile bit mask");
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ac = wid % achunks, rest = wid / achunks;
+  const int64_t tile = rest % ntiles, f = rest / ntiles;
+  if (f >= F) return;                                   // wave-uniform
+  const int64_t a = ac * 64 + lane;
+  const bool ok = a < A;
+  const double* x = X + f * D * ld + (ok ? a : A - 1);
+  const uint8_t* pres = present ? present + (ok ? a : A - 1) : nullptr;
+  const int Di = (int)D;
+  const int d0 = (int)tile * T;
+  const int d1 = min(Di, d0 + T);
+  // the tile's own rows: presence bits and (rank) the values being ranked
+  unsigned pm = 0;
+  double v[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int d = d0 + t;
+    const bool in = d < d1;
+    v[t] = (OP == FMX_TS_RANK && in) ? x[(int64_t)d * ld] : 0.0;
+    if (in && (pres == nullptr || pres[(int64_t)d * ld] != 0)) pm |= 1u << t;
+  }
+  // window start s: the (W-1)th present row before d0 (or the column's first row)
+  int pre, s;
+  if (pres == nullptr) {
+    pre = min(W - 1, d0);
+    s = d0 - pre;
+  } else {
+    pre = 0;
+    s = d0;
+    for (int db = d0 - 1;; db -= 8) {
+      const bool need = ok && pre < W - 1 && db >= 0;
+      if (__ballot(need) == 0) break;
+      uint8_t pb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pb[k] = (db - k >= 0) ? pres[(int64_t)(db - k) * ld] : 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (need && pre < W - 1 && pb[k]) { ++pre; s = db - k; }
+    }
+  }
+  // q_t - W for each present output (q_t = its present-row index counted from s)
+  double qW[T];
+  {
+    int q = pre;
+#pragma unroll
+    for (int t = 0; t < T; ++t) { qW[t] = (double)(q - W); q += (pm >> t) & 1u; }
+  }
+  double acc[T];
+  int s2[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) { acc[t] = 0.0; s2[t] = 0; }
+  const double Wd = (double)W;
+  const int smin = wave_min_i(ok ? s : d0);
+  double pd = 0.0;                                      // present index of the next row
+  for (int db = smin; db < d1; db += 8) {
+    double u[8];
+    bool pu[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int d = db + k;
+      u[k] = d < d1 ? x[(int64_t)d * ld] : 0.0;
+      pu[k] = d < d1 && d >= s && (pres == nullptr || pres[(int64_t)d * ld] != 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (!pu[k]) continue;
+      const double uk = u[k];
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const double kk = pd - qW[t];                   // weight of row p in output t's window
+        const bool inw = kk >= 1.0 && kk <= Wd;
+        if (OP == FMX_TS_DECAY) {
+          acc[t] = inw ? __builtin_fma(uk, kk, acc[t]) : acc[t];
+        } else {
+          const int inc = uk < v[t] ? 2 : (uk == v[t] ? 1 : 0);
+          const int nx = (uk != uk) ? (s2[t] | TSW_NANBIT) : (s2[t] + inc);
+          s2[t] = inw ? nx : s2[t];
+        }
+      }
+      pd += 1.0;
+    }
+  }
+  if (!ok) return;
+  double* y = Y + f * D * ld + a;
+  const double den = (double)W * (double)(W + 1) / 2.0;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int d = d0 + t;
+    if (d >= d1) break;
+    double o = qnan();
+    if (((pm >> t) & 1u) && qW[t] >= -1.0) {            // a full window of W present rows
+      if (OP == FMX_TS_DECAY) o = acc[t] / den;         // NaN in the window propagates
+      else if (s2[t] < TSW_NANBIT) o = ((double)(s2[t] + 1) / 2.0) / Wd;
+    }
+    y[(int64_t)d * ld] = o;
   }
 }
 
@@ -599,66 +752,7 @@ k_ts_corr_rl(const double* __restrict__ X, const double* __restrict__ Ycol, doub
   }
 }
 
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-// One lane owns V adjacent assets of one factor (V = 2: 16-byte loads/stores) and walks
-// the dates with TS_UNROLL rows of loads in flight.
-template <int OP, int V>
-__global__ void __launch_bounds__(TS_BLOCK)
-k_ts(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
-     int W, const uint8_t* __restrict__ present) {
-  extern __shared__ double ring[];  // [W][TS_BLOCK][V]
-  const int lane = threadIdx.x;
-  const int64_t a = ((int64_t)blockIdx.x * TS_BLOCK + lane) * V;
-  if (a >= A) return;
-  const int64_t f = blockIdx.y;
-  const double* x = X + f * D * ld + a;
-  double* y = Y + f * D * ld + a;
-  const uint8_t* pres = present ? present + a : nullptr;
-  ColState cs[V];
-#pragma unroll
-  for (int u = 0; u < V; ++u) cs[u].init();
-  for (int64_t d0 = 0; d0 < D; d0 += TS_UNROLL) {
-    double v[TS_UNROLL][V];
-    uint8_t p[TS_UNROLL][V];
-#pragma unroll
-    for (int q = 0; q < TS_UNROLL; ++q) {
-      const int64_t d = d0 + q;
-      if (d < D) {
-        if (V == 2) {
-          const dbl2 t = *reinterpret_cast<const dbl2*>(x + d * ld);
-          v[q][0] = t[0];
-          v[q][V - 1] = t[1];
-        } else {
-          v[q][0] = x[d * ld];
-        }
-#pragma unroll
-        for (int u = 0; u < V; ++u) p[q][u] = pres ? pres[d * ld + u] : 1;
-      } else {
-#pragma unroll
-        for (int u = 0; u < V; ++u) p[q][u] = 0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < TS_UNROLL; ++q) {
-      const int64_t d = d0 + q;
-      if (d >= D) continue;
-      double o[V];
-#pragma unroll
-      for (int u = 0; u < V; ++u) o[u] = p[q][u] ? ts_step<OP, V>(cs[u], v[q][u], W, ring, lane, u) : qnan();
-      if (V == 2) {
-        dbl2 t;
-        t[0] = o[0];
-        t[1] = o[V - 1];
-        *reinterpret_cast<dbl2*>(y + d * ld) = t;
-      } else {
-        y[d * ld] = o[0];
-      }
-    }
-  }
-}
-
-// W == 0: diff -> x - x, delay -> x, decay -> x (no ring).
+// W == 0: diff -> x - x, delay -> x, decay -> x (no window).
 __global__ void k_ts_window0(const double* __restrict__ X, double* __restrict__ Y, int64_t n_total,
                              int op, const uint8_t* __restrict__ present, int64_t DA, int64_t ld) {
   (void)ld;
@@ -672,82 +766,45 @@ __global__ void k_ts_window0(const double* __restrict__ X, double* __restrict__ 
   }
 }
 
-// Negative window for diff/delay: a lead by K=-W present rows.  Each row first gets NaN
-// and is overwritten once the row K steps ahead arrives.
-template <int OP>
-__global__ void __launch_bounds__(TS_BLOCK)
-k_ts_lead(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld,
-          int K, const uint8_t* __restrict__ present) {
-  extern __shared__ double ring[];  // values [K][64] then positions [K][64]
-  double* rpos = ring + (int64_t)K * TS_BLOCK;
-  const int lane = threadIdx.x;
-  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
-  if (a >= A) return;
-  const int64_t f = blockIdx.y;
-  const double* x = X + f * D * ld + a;
-  double* y = Y + f * D * ld + a;
-  int64_t i = 0;
-  int slot = 0;
-  for (int64_t d = 0; d < D; ++d) {
-    bool p = present ? present[d * ld + a] != 0 : true;
-    y[d * ld] = qnan();
-    if (!p) continue;
-    double v = x[d * ld];
-    if (i >= K) {
-      double ov = ring[slot * TS_BLOCK + lane];
-      int64_t od = (int64_t)rpos[slot * TS_BLOCK + lane];
-      y[od * ld] = (OP == FMX_TS_DIFF) ? ov - v : v;
-    }
-    ring[slot * TS_BLOCK + lane] = v;
-    rpos[slot * TS_BLOCK + lane] = (double)d;
-    slot = (slot + 1 == K) ? 0 : slot + 1;
-    i += 1;
-  }
-}
-
 // ------------------------------------------------------------------------------------
-// ts_corr (builder-defined; pandas Rolling.corr): prep_binary NaN propagation, then
-// roll_mean(x*y), roll_mean(x), roll_mean(y), roll_sum(notna) (minp 0), roll_var(x),
-// roll_var(y) and  (mxy - mx*my) * (c/(c-1)) / sqrt(vx*vy).
-__global__ void __launch_bounds__(TS_BLOCK)
-k_ts_corr(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ Out,
-          int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W,
-          const uint8_t* __restrict__ present) {
-  extern __shared__ double ring[];  // x [W][64], y [W][64]
-  double* ringy = ring + (int64_t)W * TS_BLOCK;
-  const int lane = threadIdx.x;
-  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
-  if (a >= A) return;
-  const int64_t f = blockIdx.y;
+// ts_corr (builder-defined; pandas Rolling.corr) on ragged panels: prep_binary NaN
+// propagation, then roll_mean(x*y), roll_mean(x), roll_mean(y), roll_sum(notna) (minp 0),
+// roll_var(x), roll_var(y) and  (mxy - mx*my) * (c/(c-1)) / sqrt(vx*vy).  The leaving
+// pair is re-read at the trailing row pointer (k_ts_ptr), so any W; same operation order
+// as k_ts_corr_rl: bit-identical on a fully present panel.
+__global__ void __launch_bounds__(256)
+k_ts_corr_ptr(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ Out, int64_t F,
+              int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W, const uint8_t* __restrict__ present) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
   const double* x = X + f * D * ld + a;
   const double* yc = Ycol + f * y_fstride + a;
   double* o = Out + f * D * ld + a;
+  const uint8_t* pres = present ? present + a : nullptr;
   MeanSt mxy, mx, my;
   VarSt vx, vy;
-  int64_t i = 0, cnt = 0;
-  int slot = 0;
+  int64_t i = 0, cnt = 0, tail = -1;
   bool first = true;
   for (int64_t d = 0; d < D; ++d) {
-    bool p = present ? present[d * ld + a] != 0 : true;
-    if (!p) { o[d * ld] = qnan(); continue; }
-    double xr = x[d * ld], yr = yc[d * ld];
-    double xv = xr + 0.0 * yr;
-    double yv = yr + 0.0 * xr;
-    double pv = xv * yv;
-    if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; }
+    if (pres != nullptr && pres[d * ld] == 0) { o[d * ld] = qnan(); continue; }
+    const double xr = x[d * ld], yr = yc[d * ld];
+    const double xv = xr + 0.0 * yr;
+    const double yv = yr + 0.0 * xr;
+    const double pv = xv * yv;
+    if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; tail = d; }
     if (i >= W) {
-      double ox = ring[slot * TS_BLOCK + lane], oy = ringy[slot * TS_BLOCK + lane];
+      const double txr = x[tail * ld], tyr = yc[tail * ld];
+      const double ox = txr + 0.0 * tyr, oy = tyr + 0.0 * txr;
       mxy.remove(ox * oy); mx.remove(ox); my.remove(oy); vx.remove(ox); vy.remove(oy);
       cnt -= (ox + oy == ox + oy);
+      do { ++tail; } while (pres != nullptr && pres[tail * ld] == 0);
     }
-    ring[slot * TS_BLOCK + lane] = xv;
-    ringy[slot * TS_BLOCK + lane] = yv;
-    slot = (slot + 1 == W) ? 0 : slot + 1;
     mxy.add(pv); mx.add(xv); my.add(yv); vx.add(xv); vy.add(yv);
     cnt += (xv + yv == xv + yv);
-    double c = (double)cnt;
-    double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (c / (c - 1.0));
-    double den = sqrt(vx.var(W, 1) * vy.var(W, 1));
+    const double c = (double)cnt;
+    const double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (c / (c - 1.0));
+    const double den = sqrt(vx.var(W, 1) * vy.var(W, 1));
     o[d * ld] = num / den;
     i += 1;
   }
@@ -755,39 +812,33 @@ k_ts_corr(const double* __restrict__ X, const double* __restrict__ Ycol, double*
 
 // ts_regression_fast rolling moments over the pair-valid rows of one column
 // (operations.py:204-240).  `valid` marks rows that survive the reference's dropna()
-// (y and the globally shifted x both non-NaN).  Output NaN elsewhere.
-__global__ void __launch_bounds__(TS_BLOCK)
-k_ts_regression(const double* __restrict__ Yv, const double* __restrict__ Xv,
-                const uint8_t* __restrict__ valid, double* __restrict__ Out, int64_t D, int64_t A,
-                int64_t ld, int W, int rettype) {
-  extern __shared__ double ring[];  // x [W][64], y [W][64]
-  double* ringy = ring + (int64_t)W * TS_BLOCK;
-  const int lane = threadIdx.x;
-  const int64_t a = (int64_t)blockIdx.x * TS_BLOCK + lane;
+// (y and the globally shifted x both non-NaN); output NaN elsewhere.  The leaving pair is
+// re-read at the trailing valid-row pointer: any W.
+__global__ void __launch_bounds__(256)
+k_ts_regression_ptr(const double* __restrict__ Yv, const double* __restrict__ Xv, const uint8_t* __restrict__ valid,
+                    double* __restrict__ Out, int64_t D, int64_t A, int64_t ld, int W, int rettype) {
+  const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (a >= A) return;
   MeanSt mx, my, mxx, mxy, myy;
-  int64_t i = 0;
-  int slot = 0;
+  int64_t i = 0, tail = -1;
   bool first = true;
   for (int64_t d = 0; d < D; ++d) {
-    int64_t off = d * ld + a;
+    const int64_t off = d * ld + a;
     if (!valid[off]) { Out[off] = qnan(); continue; }
-    double xv = Xv[off], yv = Yv[off];
-    if (first) { mx.init(xv); my.init(yv); mxx.init(xv * xv); mxy.init(xv * yv); myy.init(yv * yv); first = false; }
+    const double xv = Xv[off], yv = Yv[off];
+    if (first) { mx.init(xv); my.init(yv); mxx.init(xv * xv); mxy.init(xv * yv); myy.init(yv * yv); first = false; tail = d; }
     if (i >= W) {
-      double ox = ring[slot * TS_BLOCK + lane], oy = ringy[slot * TS_BLOCK + lane];
+      const double ox = Xv[tail * ld + a], oy = Yv[tail * ld + a];
       mx.remove(ox); my.remove(oy); mxx.remove(ox * ox); mxy.remove(ox * oy); myy.remove(oy * oy);
+      do { ++tail; } while (valid[tail * ld + a] == 0);
     }
-    ring[slot * TS_BLOCK + lane] = xv;
-    ringy[slot * TS_BLOCK + lane] = yv;
-    slot = (slot + 1 == W) ? 0 : slot + 1;
     mx.add(xv); my.add(yv); mxx.add(xv * xv); mxy.add(xv * yv); myy.add(yv * yv);
-    double Mx = mx.result(W), My = my.result(W);
-    double cov = mxy.result(W) - Mx * My;
-    double var_x = mxx.result(W) - Mx * Mx;
-    double beta = cov / var_x;
-    double alpha = My - beta * Mx;
-    double fitted = alpha + beta * xv;
+    const double Mx = mx.result(W), My = my.result(W);
+    const double cov = mxy.result(W) - Mx * My;
+    const double var_x = mxx.result(W) - Mx * Mx;
+    const double beta = cov / var_x;
+    const double alpha = My - beta * Mx;
+    const double fitted = alpha + beta * xv;
     double r;
     switch (rettype) {
       case 0: r = yv - fitted; break;
@@ -795,7 +846,7 @@ k_ts_regression(const double* __restrict__ Yv, const double* __restrict__ Xv,
       case 2: r = beta; break;
       case 3: r = fitted; break;
       default: {
-        double var_y = myy.result(W) - My * My;
+        const double var_y = myy.result(W) - My * My;
         r = (cov * cov) / (var_x * var_y);
       }
     }
@@ -830,13 +881,34 @@ static const void* ts_reg_kernel(int op, int W) {
   }
 }
 
-static fmx_status launch_ring(const void* kern, dim3 grid, size_t lds, hipStream_t st, void** args) {
-  if (lds > 160 * 1024) {
-    set_error("window too large for the LDS ring (needs " + std::to_string(lds) + " bytes)");
-    return FMX_ERR_UNSUPPORTED;
+template <int PF>
+static const void* ts_col_for(int op, bool ptr) {
+  switch (op) {
+    case FMX_TS_SUM: return ptr ? (const void*)k_ts_ptr<FMX_TS_SUM, PF> : (const void*)k_ts_rl<FMX_TS_SUM, PF>;
+    case FMX_TS_MEAN: return ptr ? (const void*)k_ts_ptr<FMX_TS_MEAN, PF> : (const void*)k_ts_rl<FMX_TS_MEAN, PF>;
+    case FMX_TS_STD: return ptr ? (const void*)k_ts_ptr<FMX_TS_STD, PF> : (const void*)k_ts_rl<FMX_TS_STD, PF>;
+    case FMX_TS_VAR: return ptr ? (const void*)k_ts_ptr<FMX_TS_VAR, PF> : (const void*)k_ts_rl<FMX_TS_VAR, PF>;
+    case FMX_TS_ZSCORE:
+      return ptr ? (const void*)k_ts_ptr<FMX_TS_ZSCORE, PF> : (const void*)k_ts_rl<FMX_TS_ZSCORE, PF>;
+    case FMX_TS_DIFF: return ptr ? (const void*)k_ts_ptr<FMX_TS_DIFF, PF> : (const void*)k_ts_rl<FMX_TS_DIFF, PF>;
+    case FMX_TS_DELAY: return ptr ? (const void*)k_ts_ptr<FMX_TS_DELAY, PF> : (const void*)k_ts_rl<FMX_TS_DELAY, PF>;
+    case FMX_TS_BACKFILL: return (const void*)k_ts_ptr<FMX_TS_BACKFILL, PF>;
+    default: return nullptr;
   }
-  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  FMX_HIP(hipLaunchKernel(kern, grid, dim3(TS_BLOCK), args, lds, st));
+}
+
+// k_ts_win launch: one wave per (factor, tile of TSW_T dates, 64 assets), 4 waves a block.
+static fmx_status launch_ts_win(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
+                                int W, const uint8_t* present, hipStream_t st) {
+  FMX_ARG(D < (int64_t)1 << 30, "too many dates for the windowed kernel");
+  int64_t achunks = ceil_div(A, 64), ntiles = ceil_div(D, TSW_T);
+  const int64_t waves = F * ntiles * achunks;
+  FMX_ARG(ceil_div(waves, 4) < (int64_t)1 << 31, "panel too large for one windowed launch");
+  const void* k = op == FMX_TS_RANK ? (const void*)k_ts_win<FMX_TS_RANK, TSW_T>
+                                    : (const void*)k_ts_win<FMX_TS_DECAY, TSW_T>;
+  void* args[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W,
+                  (void*)&present, (void*)&achunks, (void*)&ntiles};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)ceil_div(waves, 4)), dim3(256), args, 0, st));
   return FMX_OK;
 }
 
@@ -844,6 +916,12 @@ static fmx_status launch_ring(const void* kern, dim3 grid, size_t lds, hipStream
 
 using namespace fmx;
 
+// Dispatch (no window cap anywhere):
+//   dense, W in {5, 10, 20}          -> k_ts_reg (register ring)
+//   rank / decay otherwise           -> k_ts_win (date tiles; dense or ragged)
+//   other ops, dense                 -> k_ts_rl  (leaving value re-read at d - W)
+//   other ops, ragged; backfill      -> k_ts_ptr (trailing row pointer)
+//   diff / delay with W < 0 (a lead) -> k_ts_lead_ptr
 extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
                                 int64_t ld, int32_t window, const uint8_t* present, void* stream) {
   FMX_ARG(X && Y, "null panel");
@@ -868,57 +946,33 @@ extern "C" fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t 
     FMX_LAUNCH_CHECK("k_ts_window0");
     return FMX_OK;
   }
-  // two adjacent assets per lane (16-byte accesses) when rows stay 16-byte aligned
-  const bool v2 = (ld % 2 == 0) && (A % 2 == 0) && ((uintptr_t)X % 16 == 0) && ((uintptr_t)Y % 16 == 0) &&
-                  (getenv("FMX_TS_V1") == nullptr);
-  const int V = v2 ? 2 : 1;
-  dim3 grid((unsigned)ceil_div(A, TS_BLOCK * V), (unsigned)F);
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&W, (void*)&present};
+  const dim3 cgrid((unsigned)ceil_div(F * A, 256));
   if ((op == FMX_TS_DIFF || op == FMX_TS_DELAY) && W < 0) {
-    grid = dim3((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
+    FMX_ARG(W > INT32_MIN, "window out of range");
     int K = -W;
-    size_t lds = (size_t)2 * K * TS_BLOCK * sizeof(double);
-    const void* k = op == FMX_TS_DIFF ? (const void*)k_ts_lead<FMX_TS_DIFF> : (const void*)k_ts_lead<FMX_TS_DELAY>;
-    void* largs[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&K, (void*)&present};
-    return launch_ring(k, grid, lds, st, largs);
+    const void* k = op == FMX_TS_DIFF ? (const void*)k_ts_lead_ptr<FMX_TS_DIFF> : (const void*)k_ts_lead_ptr<FMX_TS_DELAY>;
+    void* largs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&K, (void*)&present};
+    FMX_HIP(hipLaunchKernel(k, cgrid, dim3(256), largs, 0, st));
+    return FMX_OK;
   }
   FMX_ARG(W >= 1, "window must be >= 1");
-  if (!present && op != FMX_TS_BACKFILL && getenv("FMX_TS_LDS") == nullptr) {
+  if (!present && op != FMX_TS_BACKFILL) {
     const void* kr = ts_reg_kernel(op, W);
     if (kr) {
       void* rargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld};
-      FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, st));
-      return FMX_OK;
-    }
-    // other windows: the leaving value is re-read instead of kept in a ring
-    const void* kl = op == FMX_TS_SUM ? (const void*)k_ts_rl<FMX_TS_SUM, 8>
-                   : op == FMX_TS_MEAN ? (const void*)k_ts_rl<FMX_TS_MEAN, 8>
-                   : op == FMX_TS_STD ? (const void*)k_ts_rl<FMX_TS_STD, 8>
-                   : op == FMX_TS_VAR ? (const void*)k_ts_rl<FMX_TS_VAR, 8>
-                   : op == FMX_TS_ZSCORE ? (const void*)k_ts_rl<FMX_TS_ZSCORE, 8> : nullptr;
-    if (kl && W >= 1) {
-      void* rargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W};
-      FMX_HIP(hipLaunchKernel(kl, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, st));
+      FMX_HIP(hipLaunchKernel(kr, cgrid, dim3(256), rargs, 0, st));
       return FMX_OK;
     }
   }
-  size_t lds = (op == FMX_TS_BACKFILL) ? 0 : (size_t)W * TS_BLOCK * V * sizeof(double);
-  const void* k = nullptr;
-#define FMX_TSK(O) (V == 2 ? (const void*)k_ts<O, 2> : (const void*)k_ts<O, 1>)
-  switch (op) {
-    case FMX_TS_SUM: k = FMX_TSK(FMX_TS_SUM); break;
-    case FMX_TS_MEAN: k = FMX_TSK(FMX_TS_MEAN); break;
-    case FMX_TS_STD: k = FMX_TSK(FMX_TS_STD); break;
-    case FMX_TS_VAR: k = FMX_TSK(FMX_TS_VAR); break;
-    case FMX_TS_ZSCORE: k = FMX_TSK(FMX_TS_ZSCORE); break;
-    case FMX_TS_RANK: k = FMX_TSK(FMX_TS_RANK); break;
-    case FMX_TS_DECAY: k = FMX_TSK(FMX_TS_DECAY); break;
-    case FMX_TS_DIFF: k = FMX_TSK(FMX_TS_DIFF); break;
-    case FMX_TS_DELAY: k = FMX_TSK(FMX_TS_DELAY); break;
-    default: k = FMX_TSK(FMX_TS_BACKFILL); break;
+  if (op == FMX_TS_RANK || op == FMX_TS_DECAY) return launch_ts_win(op, X, Y, F, D, A, ld, W, present, st);
+  if (!present && op != FMX_TS_BACKFILL) {
+    void* rargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W};
+    FMX_HIP(hipLaunchKernel(ts_col_for<8>(op, false), cgrid, dim3(256), rargs, 0, st));
+    return FMX_OK;
   }
-#undef FMX_TSK
-  return launch_ring(k, grid, lds, st, args);
+  void* pargs[] = {(void*)&X, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W, (void*)&present};
+  FMX_HIP(hipLaunchKernel(ts_col_for<8>(op, true), cgrid, dim3(256), pargs, 0, st));
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, double* Yzscore, double* Yrank,
@@ -955,20 +1009,20 @@ extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* O
   FMX_ARG(window >= 1, "window must be >= 1");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   int W = window;
-  if (!present && getenv("FMX_TS_LDS") == nullptr) {   // dense: leaving values re-read
+  const dim3 grid((unsigned)ceil_div(F * A, 256));
+  if (!present) {   // dense: leaving values re-read at d - W
     void* rargs[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
                      (void*)&y_fstride, (void*)&W};
     // two dates of the four streams in flight: 116 VGPRs, 4 waves/SIMD (four dates: 154
     // VGPRs, 3 waves, 160 vs 156 ms at C5; eight: 180 ms; forcing 4-5 waves spills)
     const void* kc = (const void*)k_ts_corr_rl<2>;
-    FMX_HIP(hipLaunchKernel(kc, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), rargs, 0, as_stream(stream)));
+    FMX_HIP(hipLaunchKernel(kc, grid, dim3(256), rargs, 0, as_stream(stream)));
     return FMX_OK;
   }
-  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), (unsigned)F);
-  size_t lds = (size_t)2 * W * TS_BLOCK * sizeof(double);
-  void* args[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,
+  void* args[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
                   (void*)&y_fstride, (void*)&W, (void*)&present};
-  return launch_ring((const void*)k_ts_corr, grid, lds, as_stream(stream), args);
+  FMX_HIP(hipLaunchKernel((const void*)k_ts_corr_ptr, grid, dim3(256), args, 0, as_stream(stream)));
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, double* Y, int64_t F, int64_t D,
@@ -995,9 +1049,9 @@ extern "C" fmx_status fmx_ts_regression(const double* Yv, const double* Xv, cons
   if (D == 0 || A == 0) return FMX_OK;
   int W = window;
   int rt = rettype;
-  dim3 grid((unsigned)ceil_div(A, TS_BLOCK), 1);
-  size_t lds = (size_t)2 * W * TS_BLOCK * sizeof(double);
   void* args[] = {(void*)&Yv, (void*)&Xv, (void*)&valid, (void*)&Out, (void*)&D, (void*)&A, (void*)&ld,
                   (void*)&W, (void*)&rt};
-  return launch_ring((const void*)k_ts_regression, grid, lds, as_stream(stream), args);
+  FMX_HIP(hipLaunchKernel((const void*)k_ts_regression_ptr, dim3((unsigned)ceil_div(A, 256)), dim3(256), args, 0,
+                          as_stream(stream)));
+  return FMX_OK;
 }

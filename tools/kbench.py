@@ -73,12 +73,34 @@ def _rank2(X):
     return _RK["rk"]
 
 
+_PR = {}
+
+
+def _pres(X):
+    """a ragged presence mask (10 % of rows absent), made once."""
+    if "p" not in _PR:
+        g = torch.Generator(device="cpu").manual_seed(5)
+        _PR["p"] = (torch.rand(X.shape[1:], generator=g) > 0.1).to(torch.uint8).to(X.device)
+    return _PR["p"]
+
+
 OPS = {
     "ts_mean": (lambda X, R, Y: E.ts("mean", X, 20, out=Y), 16),
     "ts_std": (lambda X, R, Y: E.ts("std", X, 20, out=Y), 16),
     "ts_zscore": (lambda X, R, Y: E.ts("zscore", X, 20, out=Y), 16),
     "ts_rank": (lambda X, R, Y: E.ts("rank", X, 10, out=Y), 16),
     "ts_decay": (lambda X, R, Y: E.ts("decay", X, 20, out=Y), 16),
+    # long windows (any W: k_ts_win tiles for rank / decay, k_ts_rl / k_ts_ptr for moments)
+    "ts_decay80": (lambda X, R, Y: E.ts("decay", X, 80, out=Y), 16),
+    "ts_decay150": (lambda X, R, Y: E.ts("decay", X, 150, out=Y), 16),
+    "ts_decay350": (lambda X, R, Y: E.ts("decay", X, 350, out=Y), 16),
+    "ts_rank60": (lambda X, R, Y: E.ts("rank", X, 60, out=Y), 16),
+    "ts_rank200": (lambda X, R, Y: E.ts("rank", X, 200, out=Y), 16),
+    "ts_mean175": (lambda X, R, Y: E.ts("mean", X, 175, out=Y), 16),
+    "ts_mean20_rg": (lambda X, R, Y: E.ts("mean", X, 20, present=_pres(X), out=Y), 16),
+    "ts_std175_rg": (lambda X, R, Y: E.ts("std", X, 175, present=_pres(X), out=Y), 16),
+    "ts_decay150_rg": (lambda X, R, Y: E.ts("decay", X, 150, present=_pres(X), out=Y), 16),
+    "ts_rank10_rg": (lambda X, R, Y: E.ts("rank", X, 10, present=_pres(X), out=Y), 16),
     "cs_rank": (lambda X, R, Y: E.cs_rank(X, out=Y), 16),
     "cs_zscore": (lambda X, R, Y: E.cs_moment("zscore", X, out=Y), 16),
     "market_neutralize": (lambda X, R, Y: E.cs_moment("market_neutralize", X, out=Y), 16),
