@@ -76,29 +76,16 @@ def ledoit_wolf_shrinkage(returns):
     return lam * target + (1 - lam) * sample_cov
 
 
-_REF_FSM = None
-
-
 def mvo_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window, risk_aversion=1.0,
                  max_weight=1.0, turnover_penalty=0.0, previous_weights=None, use_shrinkage=True, **kwargs):
     """Mean-variance factor weights (factor_selection_methods.py:119-175): a host cvxpy QP,
     outside the GPU scope.  Handed to the reference's own selector, loaded by path from
-    ``$FMX_REFERENCE_DIR`` (as the drop-in ``Simulation`` does for its MVO methods), so the
-    solver setup is the reference's exactly; it needs cvxpy like the reference."""
-    global _REF_FSM
-    if _REF_FSM is None:
-        import importlib.util
-        import os
-        d = os.environ.get("FMX_REFERENCE_DIR")
-        path = os.path.join(d, "factor_selection_methods.py") if d else None
-        if not path or not os.path.exists(path):
-            raise NotImplementedError("mvo_selector runs the reference's host QP: set FMX_REFERENCE_DIR to the "
-                                      "FactorModeling checkout that holds factor_selection_methods.py")
-        spec = importlib.util.spec_from_file_location("_fmx_reference_factor_selection_methods", path)
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
-        _REF_FSM = mod
-    return _REF_FSM.mvo_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window,
+    ``$FMX_REFERENCE_DIR`` (``_refload``, as the drop-in ``Simulation`` does for its MVO
+    methods), so the solver setup is the reference's exactly; it needs cvxpy like the
+    reference."""
+    from . import _refload
+    mod = _refload.load("factor_selection_methods.py", "mvo_selector")
+    return mod.mvo_selector(metrics_df, factors_win, returns_win, factor_ret_win, today, window,
                                  risk_aversion=risk_aversion, max_weight=max_weight,
                                  turnover_penalty=turnover_penalty, previous_weights=previous_weights,
                                  use_shrinkage=use_shrinkage, **kwargs)

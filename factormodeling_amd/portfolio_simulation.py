@@ -23,15 +23,13 @@ from ``portfolio_analyzer`` when ``run()`` needs it.
 """
 from __future__ import annotations
 
-import importlib.util
-import os
-import sys
 from dataclasses import dataclass
 
 import numpy as np
 import pandas as pd
 import torch
 
+from . import _refload
 from . import engine as E
 from .panel import device
 from .simulation import daily_trade_list
@@ -65,29 +63,12 @@ class SimulationSettings:
     return_weight: float = 0.0
 
 
-_REF_MODULE = None
-
-
 def reference_simulation_classes():
     """(Simulation, SimulationSettings) of the reference's ``portfolio_simulation.py``,
-    loaded by path from ``$FMX_REFERENCE_DIR`` under a private module name (cached).  Its
-    own imports (``portfolio_analyzer``, cvxpy, scipy) resolve as in the reference checkout;
-    the directory is appended to ``sys.path`` for ``portfolio_analyzer`` if needed."""
-    global _REF_MODULE
-    if _REF_MODULE is None:
-        d = os.environ.get("FMX_REFERENCE_DIR")
-        path = os.path.join(d, "portfolio_simulation.py") if d else None
-        if not path or not os.path.exists(path):
-            raise NotImplementedError(
-                "methods 'mvo' / 'mvo_turnover' run the reference's host QP solvers: set FMX_REFERENCE_DIR to the "
-                "FactorModeling checkout that holds portfolio_simulation.py")
-        if d not in sys.path:
-            sys.path.append(d)
-        spec = importlib.util.spec_from_file_location("_fmx_reference_portfolio_simulation", path)
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
-        _REF_MODULE = mod
-    return _REF_MODULE.Simulation, _REF_MODULE.SimulationSettings
+    loaded by path from ``$FMX_REFERENCE_DIR`` under a private module name (cached;
+    ``_refload``: the directory is on ``sys.path`` only while the module body runs)."""
+    mod = _refload.load("portfolio_simulation.py", "methods 'mvo' / 'mvo_turnover'")
+    return mod.Simulation, mod.SimulationSettings
 
 
 class _Grid:

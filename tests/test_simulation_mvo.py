@@ -26,9 +26,10 @@ def refdir(monkeypatch):
     except ImportError:
         monkeypatch.setitem(sys.modules, "cvxpy", types.ModuleType("cvxpy"))
     monkeypatch.setenv("FMX_REFERENCE_DIR", REF)
-    monkeypatch.setattr(sys, "path", list(sys.path))       # the loader appends REF
+    monkeypatch.setattr(sys, "path", list(sys.path))
+    import factormodeling_amd._refload as RL
     import factormodeling_amd.portfolio_simulation as PS
-    monkeypatch.setattr(PS, "_REF_MODULE", None)
+    monkeypatch.setattr(RL, "_CACHE", {})
     sys.dont_write_bytecode = True
     return PS
 
@@ -63,6 +64,8 @@ def test_mvo_trade_list_through_dropin_matches_reference(refdir, method):
     w_ref, counts_ref = ref._daily_trade_list()
     pd.testing.assert_series_equal(w, w_ref)
     pd.testing.assert_frame_equal(counts, counts_ref)
+    # the reference directory was on sys.path only while its module body ran
+    assert REF not in sys.path
     # the QP really ran (not the equal-weight fallback): weights are not all +-1/k
     nz = w.dropna()
     nz = nz[nz != 0]
@@ -70,9 +73,10 @@ def test_mvo_trade_list_through_dropin_matches_reference(refdir, method):
 
 
 def test_mvo_without_reference_dir_fails_loudly(monkeypatch):
+    import factormodeling_amd._refload as RL
     import factormodeling_amd.portfolio_simulation as PS
     monkeypatch.delenv("FMX_REFERENCE_DIR", raising=False)
-    monkeypatch.setattr(PS, "_REF_MODULE", None)
+    monkeypatch.setattr(RL, "_CACHE", {})
     s, feat = _settings(PS.SimulationSettings, "mvo")
     with pytest.raises(NotImplementedError, match="FMX_REFERENCE_DIR"):
         PS.Simulation("sig", feat, s)._daily_trade_list()
