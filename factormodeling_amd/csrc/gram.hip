@@ -1261,8 +1261,8 @@ __device__ __forceinline__ void gw_tile(int t, int64_t F, int& bi, int& bj) {
 template <bool VEC>
 __global__ void __launch_bounds__(1024)
 k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
-            int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t ntile, int64_t nslice, int xcd, int opt,
-            double* __restrict__ part, uint16_t* __restrict__ bits16, int64_t nwd) {
+            int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t phase, int64_t ntile, int64_t nslice, int xcd,
+            int opt, double* __restrict__ part, uint16_t* __restrict__ bits16, int64_t nwd) {
   extern __shared__ double gsm[];             // [2][As (256 x KP) | Bs (128 x KP)]
   constexpr int BUF = (GW_I + GW_J) * GW_KP;
   // work item = slice * ntile + tile.  xcd: workgroups are dealt round-robin to the 8 XCDs,
@@ -1280,8 +1280,10 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   int bi, bj;
   gw_tile((int)tile, F, bi, bj);
   const int i0 = bi * GW_I, j0 = bj * GW_J;
-  const int64_t ds = d0 + slice * dates_per_slice;
-  const int64_t de = min<int64_t>(d1, ds + dates_per_slice);
+  // slice s: dates [d0 + s dps - phase, d0 + (s + 1) dps - phase) clipped to [d0, d1); a
+  // nonzero phase aligns the slices to ABSOLUTE date blocks (fmx_gram_direct_exact)
+  const int64_t ds = slice == 0 ? d0 : d0 + slice * dates_per_slice - phase;
+  const int64_t de = min<int64_t>(d1, d0 + (slice + 1) * dates_per_slice - phase);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   dbl4 acc[4][2];
@@ -1505,6 +1507,33 @@ __global__ void k_gram_counts(const unsigned long long* __restrict__ ncnt, int64
   N[j * F + i] = n;
 }
 
+// Exact fold of k_gram_f64w's block partials (fmx_gram_direct_exact): element e of tile
+// `tile` (i <= j < F) adds its nslice partials into fixed-point limbs in registers (ex_add)
+// and stores / adds them to limbs [EX_SLOTS][F][F]; its pair count from ncnt likewise.  Every
+// (i <= j) lies in exactly one tile: one writer per element, no atomics.
+__global__ void __launch_bounds__(256)
+k_gram_fold_w(const double* __restrict__ part, int64_t nslice, int64_t ntile, int64_t F,
+              const unsigned long long* __restrict__ ncnt, int64_t* __restrict__ limbs,
+              int64_t* __restrict__ counts, int accumulate) {
+  const int64_t tile = blockIdx.x;
+  int bi, bj;
+  gw_tile((int)tile, F, bi, bj);
+  const int e = blockIdx.y * blockDim.x + threadIdx.x;
+  if (e >= GW_I * GW_J) return;
+  const int64_t i = (int64_t)bi * GW_I + e / GW_J, j = (int64_t)bj * GW_J + e % GW_J;
+  if (i > j || j >= F) return;
+  int64_t acc[EX_SLOTS];
+#pragma unroll
+  for (int k = 0; k < EX_SLOTS; ++k) acc[k] = 0;
+  const double* p = part + tile * (GW_I * GW_J) + e;
+#pragma unroll 4
+  for (int64_t sl = 0; sl < nslice; ++sl) ex_add(acc, p[sl * ntile * (GW_I * GW_J)]);
+  const int64_t FF = F * F, o = i * F + j;
+#pragma unroll
+  for (int k = 0; k < EX_SLOTS; ++k) limbs[k * FF + o] = (accumulate ? limbs[k * FF + o] : 0) + acc[k];
+  counts[o] = (accumulate ? counts[o] : 0) + (int64_t)ncnt[o];
+}
+
 }  // namespace fmx
 
 struct DirectPlan {
@@ -1588,9 +1617,10 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   int64_t nwd = pl.nwd;
   static const int wopt = [] { const char* e = getenv("FMX_GRAM_WOPT"); return e ? atoi(e) : 1; }();
   int wopt_arg = wopt;
+  int64_t phase = 0;
   void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
-                  (void*)&dps, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg, (void*)&part,
-                  (void*)&bits16, (void*)&nwd};
+                  (void*)&dps, (void*)&phase, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg,
+                  (void*)&part, (void*)&bits16, (void*)&nwd};
   const dim3 grid = xcd == 2 ? dim3((unsigned)ntile, (unsigned)nslice) : dim3((unsigned)nwg);
   FMX_HIP(hipLaunchKernel(k, grid, dim3(1024), args, lds, st));
   k_gram_reduce_w<<<dim3((unsigned)pl.g.ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, pl.g.nslice, pl.g.ntile, F,
@@ -1606,6 +1636,84 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
   FMX_LAUNCH_CHECK("k_gram_popc_fm");
   k_gram_counts<<<(unsigned)ceil_div(F * F, (int64_t)256), 256, 0, st>>>(ncnt, F, N, accumulate);
   FMX_LAUNCH_CHECK("k_gram_counts");
+  return FMX_OK;
+}
+
+// Exact (GPU-count-independent) direct Gram: the tile kernel's date slices are ABSOLUTE
+// blocks of FMX_GRAM_DATE_BLOCK dates (local row 0 = absolute date d_origin), each block's
+// fp64 partial tiles fold into fixed-point limbs (exactsum.hpp).  A date shard whose bounds
+// are multiples of the block holds whole blocks, so every block's partial -- and the integer
+// sum over blocks and ranks -- is the same at 1, 2, 4 or 8 GPUs.
+static DirectPlan direct_exact_plan(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int64_t phase) {
+  DirectPlan p;
+  p.F = F;
+  p.D = D;
+  p.g.nb = 0;
+  p.g.ntile = gw_ntile(F);
+  p.g.dps = FMX_GRAM_DATE_BLOCK;
+  p.g.nslice = ceil_div(d1 - d0 + phase, (int64_t)FMX_GRAM_DATE_BLOCK);
+  p.nd = d1 - d0;
+  p.nwd = ceil_div(A, (int64_t)32);
+  p.nw = p.nd * p.nwd;
+  return p;
+}
+
+static int64_t block_phase(int64_t d_origin, int64_t d0) {
+  const int64_t a = d_origin + d0;
+  return ((a % FMX_GRAM_DATE_BLOCK) + FMX_GRAM_DATE_BLOCK) % FMX_GRAM_DATE_BLOCK;
+}
+
+extern "C" int64_t fmx_gram_direct_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1,
+                                                    int64_t d_origin) {
+  if (F <= 0 || d1 <= d0) return 0;
+  return direct_exact_plan(F, D, A, d0, d1, block_phase(d_origin, d0)).bytes();
+}
+
+extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts,
+                                            int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
+                                            int64_t d_origin, int32_t accumulate, void* work, int64_t work_bytes,
+                                            void* stream) {
+  FMX_ARG(X && stats && limbs && counts, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1 && d_origin >= 0, "bad dims");
+  FMX_ARG(F <= 65535 && d1 - d0 <= 0x7fffffff, "too many factors / dates");
+  hipStream_t st = as_stream(stream);
+  if (!accumulate && F > 0) {
+    FMX_HIP(hipMemsetAsync(limbs, 0, sizeof(int64_t) * FMX_GRAM_EXACT_SLOTS * F * F, st));
+    FMX_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * F * F, st));
+  }
+  if (F == 0 || d1 == d0 || A == 0) return FMX_OK;
+  const int64_t phase = block_phase(d_origin, d0);
+  const DirectPlan pl = direct_exact_plan(F, D, A, d0, d1, phase);
+  if (fmx_status e = check_work(work, work_bytes, pl.bytes(), "fmx_gram_direct_exact_work_bytes")) return e;
+  char* w = static_cast<char*>(work);
+  uint32_t* bits = reinterpret_cast<uint32_t*>(w);
+  double* part = reinterpret_cast<double*>(w + pl.bits_bytes());
+  unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
+  double* zinv = reinterpret_cast<double*>(w + pl.bits_bytes() + pl.part_bytes() + SmallPlan::align256(pl.cnt_bytes()));
+  if (ceil_div(A, (int64_t)GW_K) % 2 == 1) FMX_HIP(hipMemsetAsync(bits, 0, pl.bits_bytes(), st));
+  k_inv_stats<<<(unsigned)ceil_div(F * D, (int64_t)256), 256, 0, st>>>(stats, zinv, F * D);
+  FMX_LAUNCH_CHECK("k_inv_stats");
+  const double* zst = zinv;
+  const void* k = (ld % 2 == 0) ? (const void*)k_gram_f64w<true> : (const void*)k_gram_f64w<false>;
+  FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAM_W_LDS));
+  int64_t dps = pl.g.dps, ntile = pl.g.ntile, nslice = pl.g.nslice, ph = phase, nwd = pl.nwd;
+  int xcd_arg = 1, wopt_arg = 1;
+  const int64_t nwg = 8 * ((ntile * nslice + 7) / 8);
+  uint16_t* bits16 = reinterpret_cast<uint16_t*>(bits);
+  void* args[] = {(void*)&X, (void*)&zst, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&d0, (void*)&d1,
+                  (void*)&dps, (void*)&ph, (void*)&ntile, (void*)&nslice, (void*)&xcd_arg, (void*)&wopt_arg,
+                  (void*)&part, (void*)&bits16, (void*)&nwd};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nwg), dim3(1024), args, GRAM_W_LDS, st));
+  FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
+  const int T = (int)ceil_div(F, (int64_t)PF_T);
+  const int ntp = T * (T + 1) / 2;
+  const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(pl.nw, (int64_t)4 * PF_W), 2048 / ntp + 1));
+  const int64_t wps = ceil_div(ceil_div(pl.nw, nks), (int64_t)PF_W) * PF_W;
+  k_gram_popc_fm<<<dim3((unsigned)ntp, (unsigned)ceil_div(pl.nw, wps)), 256, 0, st>>>(bits, F, pl.nw, wps, ncnt);
+  FMX_LAUNCH_CHECK("k_gram_popc_fm");
+  k_gram_fold_w<<<dim3((unsigned)ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, nslice, ntile, F, ncnt, limbs, counts,
+                                                                          accumulate ? 1 : 0);
+  FMX_LAUNCH_CHECK("k_gram_fold_w");
   return FMX_OK;
 }
 

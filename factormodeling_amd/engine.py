@@ -537,6 +537,37 @@ def gram_direct(X, d0=0, d1=None, stats=None):
     return G, N
 
 
+GRAM_DATE_BLOCK = 16            # fmx.h FMX_GRAM_DATE_BLOCK: date shards align to it (wide Gram)
+
+
+def gram_direct_exact(X, d0=0, d1=None, d_origin=0, stats=None, limbs=None, counts=None, accumulate=False):
+    """Exact fixed-point partials of the wide Gram over dates [d0, d1) (fmx_gram_direct_exact,
+    any F): (limbs int64 [7][F][F], counts int64 [F][F]).  Slices are absolute blocks of
+    GRAM_DATE_BLOCK dates (local row 0 = absolute date ``d_origin``), so shards aligned to
+    the block sum (int64 all-reduce) to the same bits at any GPU count; gram_exact_finalize
+    gives G, N."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    d1 = D if d1 is None else d1
+    if stats is None:
+        _, stats = cs_moment_stats("stats", X)
+    elif tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous():
+        raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
+    if limbs is None:
+        limbs = torch.empty((GRAM_EXACT_SLOTS, F, F), dtype=torch.int64, device=X.device)
+    if counts is None:
+        counts = torch.empty((F, F), dtype=torch.int64, device=X.device)
+    if tuple(limbs.shape) != (GRAM_EXACT_SLOTS, F, F) or limbs.dtype != torch.int64 or not limbs.is_contiguous() \
+            or tuple(counts.shape) != (F, F) or counts.dtype != torch.int64 or not counts.is_contiguous():
+        raise _lib.FmxError("gram_direct_exact: limbs int64 [7][F][F], counts int64 [F][F]")
+    nb = int(_lib.load().fmx_gram_direct_exact_work_bytes(F, D, A, int(d0), int(d1), int(d_origin)))
+    work, wb = _workspace_bytes(X.device, nb)
+    call("fmx_gram_direct_exact", ptr(X), ptr(stats), ptr(limbs), ptr(counts), F, D, A, A, int(d0), int(d1),
+         int(d_origin), int(bool(accumulate)), ptr(work), wb, stream_ptr())
+    return limbs, counts
+
+
 def gram_wide(X, d0=0, d1=None):
     """The wide (F > 256) Gram: direct from the panel by default; FMX_GRAM_MATERIALIZE=1
     selects the date-chunked Z / M path (A/B)."""

@@ -162,18 +162,27 @@ def synthetic_panel(D, A, F, device, seed=0, d_lo=0, d_hi=None, halo=0):
     return X, R, lo
 
 
-def shard_bounds(D, world, rank):
-    """Owned dates [d_lo, d_hi) of ``rank``: contiguous blocks of ceil(D / world) dates."""
+def shard_bounds(D, world, rank, align=1):
+    """Owned dates [d_lo, d_hi) of ``rank``: contiguous blocks of ceil(D / world) dates,
+    rounded up to a multiple of ``align`` (the wide Gram's absolute date blocks,
+    E.GRAM_DATE_BLOCK: every block then lies on one rank, so its exact partial is the same
+    at any GPU count)."""
     per = (D + world - 1) // world
+    per = (per + align - 1) // align * align
     return min(D, rank * per), min(D, (rank + 1) * per)
 
 
-def check_sharding(D, world, halo):
+def shard_align(F):
+    """Date alignment of the shards: the wide (F > 256) Gram sums absolute date blocks."""
+    return E.GRAM_DATE_BLOCK if F > E.FUSED_GRAM_MAX_F else 1
+
+
+def check_sharding(D, world, halo, align=1):
     """Every rank must own at least one date, and every rank that sends a halo (all but the
     last) at least ``halo`` dates: its last ``halo`` rows are the next rank's warm-up, and
     with fewer they would include its own not-yet-received halo rows."""
     for r in range(world):
-        lo, hi = shard_bounds(D, world, r)
+        lo, hi = shard_bounds(D, world, r, align)
         if hi - lo < 1 or (r + 1 < world and hi - lo < halo):
             raise ValueError(f"date sharding of D={D} over {world} ranks: rank {r} owns {hi - lo} dates, "
                              f"needs >= {max(1, halo) if r + 1 < world else 1} (halo {halo})")
@@ -185,7 +194,7 @@ class ShardedPanel:
     (factormodeling_amd.comm: TorchComm over RCCL / gloo, or LocalComm for in-process
     shards); by default torch.distributed's process group when one is initialised."""
 
-    def __init__(self, D, A, F, rank=None, world=None, device=None, seed=0, halo=HALO, comm=None):
+    def __init__(self, D, A, F, rank=None, world=None, device=None, seed=0, halo=HALO, comm=None, align=None):
         # halo: rolling warm-up + IC lag of the step's longest window (StepConfig.halo)
         if comm is None and world is not None and world > 1:
             from .comm import TorchComm
@@ -200,8 +209,9 @@ class ShardedPanel:
         self.comm = comm
         self.D, self.A, self.F = D, A, F
         self.rank, self.world = rank, world
-        check_sharding(D, world, halo)
-        self.d_lo, self.d_hi = shard_bounds(D, world, rank)
+        self.align = shard_align(F) if align is None else align
+        check_sharding(D, world, halo, self.align)
+        self.d_lo, self.d_hi = shard_bounds(D, world, rank, self.align)
         self.halo = halo if rank > 0 else 0
         self.halo_len = halo
         self.device = device
@@ -331,6 +341,12 @@ class EngineBackend:
         return E.gram_exact(X, stats, d0, d1)
 
     gram_exact_finalize = staticmethod(E.gram_exact_finalize)
+
+    @staticmethod
+    def corr_gram_wide_exact(X, d0, d1, d_origin, stats=None):
+        """Exact fixed-point partials of the wide Gram (any F) over local dates [d0, d1);
+        local row 0 is absolute date ``d_origin`` (slices are absolute date blocks)."""
+        return E.gram_direct_exact(X, d0, d1, d_origin, stats)
 
     @staticmethod
     def corr_gram(X, d0, d1, stats=None, z=None):
@@ -649,10 +665,14 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
 def gram_partials(sp, be, side):
     """This rank's share of the factor Gram over its owned dates: ("exact", (limbs, counts))
     -- integer fixed-point partials whose sum over ranks is independent of the GPU count
-    (F <= 256, gram_exact) -- or ("float", (G, N)) for the wide chunked path."""
+    (F <= 256: gram_exact's per-date units; wider: gram_direct_exact's absolute date blocks,
+    the shards aligned to them) -- or ("float", (G, N)) for backends without either."""
     d0, d1 = sp.halo, sp.X.shape[1]
     if hasattr(be, "corr_gram_exact") and sp.F <= E.FUSED_GRAM_MAX_F:
         return "exact", be.corr_gram_exact(sp.X, d0, d1, side.get("stats"), side.get("zscore"))
+    if hasattr(be, "corr_gram_wide_exact") and sp.d_lo % getattr(sp, "align", 1) == 0 \
+            and getattr(sp, "align", 1) % E.GRAM_DATE_BLOCK == 0:
+        return "exact", be.corr_gram_wide_exact(sp.X, d0, d1, sp.d_lo - sp.halo, side.get("stats"))
     if hasattr(be, "corr_gram"):
         return "float", be.corr_gram(sp.X, d0, d1, side.get("stats"), side.get("zscore"))
     Z, M = be.zscore_exposures(sp.X[:, d0:].contiguous())
@@ -697,8 +717,8 @@ def weighted_composite_step(sp, cfg, w, be=ENGINE, X=None):
 
 def ordered_sum(T, comm):
     """Sum of every rank's ``T`` in rank order (all-gather + sequential adds): identical on
-    every rank, but a different rounding of the sum at each GPU count.  Only the wide (F >
-    256) Gram still uses it; F <= 256 goes through the exact limbs (gram_exact)."""
+    every rank, but a different rounding of the sum at each GPU count.  Only backends
+    without the exact Gram partials use it (the CPU oracle backend in the gloo tests)."""
     parts = comm.all_gather(T.contiguous())
     acc = parts[0].clone()
     for p in parts[1:]:

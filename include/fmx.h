@@ -305,6 +305,18 @@ fmx_status fmx_gram_exact(const double* X, const double* stats, int64_t* limbs, 
                           int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int32_t accumulate, void* work,
                           int64_t work_bytes, void* stream);
 int64_t fmx_gram_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1);
+/* Exact, GPU-count-independent form of fmx_gram_direct (any F; C4's 2000 x 2000 at
+ * 2/4/8 GPUs, builder-defined A19).  The tile kernel's date slices are ABSOLUTE blocks of
+ * FMX_GRAM_DATE_BLOCK dates (local row 0 of X is absolute date d_origin); each block's fp64
+ * partial tiles fold into the same fixed-point limbs as fmx_gram_exact.  A date shard whose
+ * bounds are multiples of FMX_GRAM_DATE_BLOCK holds whole blocks, so an int64 all-reduce of
+ * limbs / counts + fmx_gram_exact_finalize gives the same G, N bits at every GPU count.
+ * accumulate = 0 zeroes limbs and counts first.  work: fmx_gram_direct_exact_work_bytes. */
+#define FMX_GRAM_DATE_BLOCK 16
+fmx_status fmx_gram_direct_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts, int64_t F,
+                                 int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int64_t d_origin,
+                                 int32_t accumulate, void* work, int64_t work_bytes, void* stream);
+int64_t fmx_gram_direct_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int64_t d_origin);
 /* G, N [F][F] (symmetric) from exact limbs / counts (N and counts may be NULL); a flagged
  * (non-finite or >= 2^127) term makes the entry NaN. */
 fmx_status fmx_gram_exact_finalize(const int64_t* limbs, const int64_t* counts, double* G, double* N, int64_t F,

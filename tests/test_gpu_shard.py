@@ -111,3 +111,79 @@ def test_gram_exact_split_invariant_on_device(dev, F, A):
     Gz, Nzf = E.gram_exact_finalize(Lz, Nz)
     np.testing.assert_allclose(Gz.cpu().numpy(), G1.cpu().numpy(), rtol=1e-12, atol=1e-9)
     assert torch.equal(Nzf, Nf1)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("F,A", [(300, 257), (520, 1000)])
+def test_gram_direct_exact_block_split_invariant(dev, F, A):
+    """fmx_gram_direct_exact (the wide Gram): any split of the dates at
+    absolute multiples of GRAM_DATE_BLOCK -- each piece a separate launch on its own local
+    panel with its d_origin -- sums (as integers) to the same limbs / counts bits as one
+    launch; G agrees with the float direct Gram and the oracle."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F + A)
+    D = 53
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.03] = np.nan
+    X[1, 7] = 2.5                                   # constant row: invalid
+    Xd = torch.as_tensor(X, device=dev)
+    L1, N1 = E.gram_direct_exact(Xd)
+    G1, Nf1 = E.gram_exact_finalize(L1, N1)
+    B = E.GRAM_DATE_BLOCK
+    for cuts in ([B], [B, 2 * B], [3 * B]):
+        b = [0] + cuts + [D]
+        L = torch.zeros_like(L1)
+        N = torch.zeros_like(N1)
+        for a0, a1 in zip(b[:-1], b[1:]):
+            h = min(a0, 5)                          # a halo of preceding rows in the local panel
+            loc = Xd[:, a0 - h:a1].contiguous()
+            la, na = E.gram_direct_exact(loc, h, loc.shape[1], d_origin=a0 - h)
+            L += la
+            N += na
+        G, Nf = E.gram_exact_finalize(L, N)
+        assert torch.equal(G, G1) and torch.equal(Nf, Nf1), cuts
+    Gf, Nff = E.gram_direct(Xd)
+    np.testing.assert_allclose(G1.cpu().numpy(), Gf.cpu().numpy(), rtol=1e-12, atol=1e-9)
+    assert torch.equal(Nf1, Nff)
+    Z, M = OG.zscore_exposures(X)
+    Zf, Mf = Z.reshape(F, -1), M.reshape(F, -1)
+    np.testing.assert_allclose(G1.cpu().numpy(), Zf @ Zf.T, rtol=1e-11, atol=1e-9)
+    assert np.array_equal(Nf1.cpu().numpy(), Mf @ Mf.T)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 3])
+def test_wide_gram_step_gpu_count_invariant(dev, world):
+    """C4-shaped step (IC order + wide Gram + greedy prune) at F = 300 over LocalComm
+    shards: C and the kept set are bit-identical to the 1-shard run (shards aligned to the
+    Gram's date blocks, exact limbs all-reduced as int64)."""
+    import torch
+    from factormodeling_amd import pipeline as PL
+    from factormodeling_amd.comm import run_local_shards
+    D, A, F = 200, 300, 300
+    cfg = PL.StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None)
+    _, kept1, col1 = _one_shard_nosel(dev, D, A, F, cfg, 5)
+
+    def shard(rank, comm):
+        sp = PL.ShardedPanel(D, A, F, device=dev, seed=5, halo=cfg.halo, comm=comm)
+        assert sp.d_lo % PL.E.GRAM_DATE_BLOCK == 0
+        col = {}
+        _, kept = PL.run_step(sp, cfg, collect=col)
+        torch.cuda.current_stream().synchronize()
+        return kept, col["C"].cpu().numpy()
+
+    for kept, C in run_local_shards(world, shard):
+        assert np.array_equal(C, col1["C"])
+        assert kept == kept1
+
+
+def _one_shard_nosel(dev, D, A, F, cfg, seed):
+    import torch
+    from factormodeling_amd import pipeline as PL
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=seed, halo=cfg.halo)
+    col = {}
+    w, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    return w, kept, {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in col.items()}

@@ -114,6 +114,15 @@ def test_shard_bounds_cover_dates():
         assert spans[0][0] == 0 and spans[-1][1] == 2520
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
     assert PL.HALO >= max(w for k, o, w in PL.OPS if w) - 1 + 2
+    # wide-Gram alignment: every rank starts on an absolute multiple of the date block
+    B = PL.E.GRAM_DATE_BLOCK
+    assert PL.shard_align(300) == B and PL.shard_align(200) == 1
+    for world in (1, 2, 3, 4, 8):
+        spans = [PL.shard_bounds(2520, world, r, B) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == 2520
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+        assert all(lo % B == 0 for lo, _ in spans)
+        PL.check_sharding(2520, world, 61, B)
 
 
 def test_rank_owning_fewer_dates_than_halo_is_rejected():
