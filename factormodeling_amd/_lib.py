@@ -65,6 +65,10 @@ SIGNATURES = {
     "fmx_gram_direct_exact": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp,
                               c_i64, c_vp],
     "fmx_gram_direct_exact_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64],
+    "fmx_ic_daily_sorted": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp],
+    "fmx_ic_daily_sorted_work_bytes": [c_i64, c_i64, c_i64],
+    "fmx_group_op_long": [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp],
+    "fmx_group_op_long_work_bytes": [c_i64, c_i64, c_i64],
     "fmx_gram_fused": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     "fmx_gram_fused_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
     "fmx_gram_exact": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
@@ -88,7 +92,8 @@ SIGNATURES = {
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64, "fmx_gram_direct_work_bytes": c_i64,
-             "fmx_gram_direct_exact_work_bytes": c_i64,
+             "fmx_gram_direct_exact_work_bytes": c_i64, "fmx_ic_daily_sorted_work_bytes": c_i64,
+             "fmx_group_op_long_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
              "fmx_cs_rank_sorted_work_bytes": c_i64, "fmx_group_rank_sorted_work_bytes": c_i64, "fmx_gram_exact_work_bytes": c_i64,
              "fmx_debug_exact_fold": None}

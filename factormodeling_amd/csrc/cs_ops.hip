@@ -1016,6 +1016,120 @@ k_group_long(const double* __restrict__ X, const int32_t* __restrict__ G, double
   }
 }
 
+// Group mean / neutralize / normalize on rows past 16,384 assets (operations.py:112-149),
+// where k_group_long's register-resident row and LDS compaction end.  The row stays in HBM
+// (L2-resident while its workgroup walks it); per group the members are compacted in asset
+// order into the workgroup's slice of a global scratch (block scan per 1024-cell chunk) and
+// reduced with the numpy pairwise schedule of their count -- the same arithmetic, in the
+// same order, as k_group_long, so the outputs are bit-identical to it.  Persistent
+// workgroups (gridDim.x of them, A doubles of scratch each) walk the (factor, date) rows.
+// Codes outside [0, ngroups) and absent cells belong to no group (NaN).
+template <int OP>
+__global__ void __launch_bounds__(GL_NT)
+k_group_xl(const double* __restrict__ X, const int32_t* __restrict__ G, double* __restrict__ Y, int64_t F, int64_t D,
+           int64_t A, int64_t ld, int ngroups, const uint8_t* __restrict__ present, PwTable pw,
+           double* __restrict__ scratch) {
+  __shared__ double nodes[2 * (65536 / 64) + 8];
+  __shared__ int iscr[GL_NW + 2];
+  const int t = threadIdx.x;
+  double* vals = scratch + (int64_t)blockIdx.x * A;
+  for (int64_t row = blockIdx.x; row < F * D; row += gridDim.x) {
+    const int64_t f = row / D, d = row % D;
+    const double* x = X + (f * D + d) * ld;
+    const int32_t* g = G + d * ld;
+    double* y = Y + (f * D + d) * ld;
+    const uint8_t* prow = present ? present + d * ld : nullptr;
+    auto code = [&](int64_t a) {
+      const int c = (!prow || prow[a]) ? g[a] : -1;
+      return (c >= 0 && c < ngroups) ? c : -1;
+    };
+    for (int64_t a = t; a < A; a += GL_NT)
+      if (code(a) < 0) y[a] = qnan();
+    for (int gg = 0; gg < ngroups; ++gg) {
+      int m = 0;
+      for (int64_t c0 = 0; c0 < A; c0 += GL_NT) {
+        const int64_t a = c0 + t;
+        const bool mem = a < A && code(a) == gg;
+        int tot;
+        const int off = block_exscan<GL_NT>(mem ? 1 : 0, iscr, &tot);
+        if (mem) vals[m + off] = x[a];
+        m += tot;
+        __syncthreads();                          // iscr reused by the next chunk's scan
+      }
+      if (m == 0) continue;                       // block-uniform
+      const int32_t* sch = pw.get(m);
+      int cnt;
+      const double s1 = block_pw_sum_w0<GL_NT>([&](int i) { const double v = vals[i]; return v == v ? v : 0.0; },
+                                               [&](int i) { return (int)(vals[i] == vals[i]); }, sch, nodes, iscr,
+                                               &cnt);
+      const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+      double sd = 0.0;
+      if (OP == 2) {
+        int c2;
+        const double s2 = block_pw_sum_w0<GL_NT>([&](int i) {
+          const double v = vals[i];
+          const double z = v == v ? v : 0.0;
+          const double q = (mean - z) * (mean - z);
+          return v == v ? q : 0.0;
+        }, [](int) { return 0; }, sch, nodes, iscr, &c2);
+        sd = sqrt(cnt > 0 ? s2 / (double)cnt : qnan());
+      }
+      const bool guard = (OP == 2) && (sd == 0.0 || sd != sd);
+      for (int64_t a = t; a < A; a += GL_NT) {
+        if (code(a) != gg) continue;
+        const double v = x[a];
+        double o;
+        if (OP == 0) o = mean;
+        else if (OP == 1) o = v - mean;
+        else o = guard ? 0.0 : (v - mean) / sd;
+        y[a] = o;
+      }
+      __syncthreads();                            // scratch reused by the next group
+    }
+  }
+}
+
+static int64_t group_xl_grid(int64_t rows) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return std::max(n, 1);
+  }();
+  return std::max<int64_t>(1, std::min<int64_t>(rows, 2 * (int64_t)cus));
+}
+
+extern "C" int64_t fmx_group_op_long_work_bytes(int64_t F, int64_t D, int64_t A) {
+  if (F <= 0 || D <= 0 || A <= 0) return 0;
+  return (int64_t)sizeof(double) * group_xl_grid(F * D) * A;
+}
+
+extern "C" fmx_status fmx_group_op_long(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F, int64_t D,
+                                        int64_t A, int64_t ld, int32_t ngroups, const uint8_t* present, void* work,
+                                        int64_t work_bytes, void* stream) {
+  FMX_ARG(X && G && Y && Y != X, "null / aliased panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  FMX_ARG(op >= FMX_GROUP_MEAN && op <= FMX_GROUP_NORMALIZE, "group mean / neutralize / normalize (rank: "
+                                                               "fmx_group_rank_sorted)");
+  FMX_ARG(ngroups >= 0, "bad group count");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  if (!work || work_bytes < fmx_group_op_long_work_bytes(F, D, A)) {
+    set_error("workspace smaller than fmx_group_op_long_work_bytes()");
+    return FMX_ERR_ARG;
+  }
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  const void* k = op == FMX_GROUP_MEAN ? (const void*)k_group_xl<0>
+                : op == FMX_GROUP_NEUTRALIZE ? (const void*)k_group_xl<1> : (const void*)k_group_xl<2>;
+  int ng = ngroups;
+  double* scr = static_cast<double*>(work);
+  void* args[] = {(void*)&X, (void*)&G, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&ng,
+                  (void*)&present, (void*)&pw, (void*)&scr};
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)group_xl_grid(F * D)), dim3(GL_NT), args, 0, as_stream(stream)));
+  return FMX_OK;
+}
+
 extern "C" fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F,
                                    int64_t D, int64_t A, int64_t ld, int32_t ngroups, int32_t method,
                                    const uint8_t* present, void* stream) {

@@ -9,6 +9,9 @@
 //   read off the sorted row.
 // * group_rank_normalized (operations.py:152-168) for groups larger than the per-group LDS
 //   sort takes (8192) or rows past 16,384: rows sorted by (group, value).
+// * the daily IC / rank IC / beta (factor_selector.py:36-48) past 16,384 assets (where the
+//   16-bit doubled ranks of the fine kernels end): ranks over each lag's pair-valid subset
+//   read off the sorted row.
 //
 // keys = order-preserving u64 of the value (sentinel for NaN / absent cells), values = the
 // asset index; rocPRIM's segmented radix sort (stable: equal keys keep ascending asset
@@ -282,6 +285,155 @@ k_rs_gkeys(const uint16_t* __restrict__ idx, const int32_t* __restrict__ G, cons
   gk[r * A + q] = (p && g >= 0 && g < ngroups) ? (uint32_t)g : 0xffffffffu;
 }
 
+// ------------------------------------------------------------------------------------
+// Daily IC of sorted rows (factor_selector.py:36-48: pairs (X[f][s], R[s + L]) with both
+// non-NaN, n < 3 -> NaN stats; IC = pearsonr(x, r), rank IC = pearsonr(rankdata(x over the
+// pairs), r), beta = x.r / x.x), one wave per row (f, s) of the chunk.  Per lag:
+//  pass 1 (left to right over the sorted valid keys): P(q) = # pairs at sorted positions < q
+//    (ballot prefix); each position's tie-run start s_q; P(s_q) to scratch; the lag's moment
+//    anchor = its first pair in sorted order;
+//  pass 2 (right to left): the run end e_q (next run start), so a pair's doubled average rank
+//    over the pairs is 2 * #less + #equal + 1 = P(s_q) + P(e_q) + 1; sums of x', r', x'^2,
+//    r'^2, x'r' about the anchor, of 2k * r' and (2k)^2 (exact integers) -- the same
+//    single-pass shifted moments and record formulas as k_ic_wave (~1e-15 relative to the
+//    two-pass scipy arithmetic).
+__device__ __forceinline__ double rs_wsum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(64 * RS_WPB)
+k_rs_ic(const uint64_t* __restrict__ keys, const uint16_t* __restrict__ idx, uint32_t* __restrict__ scratch,
+        const double* __restrict__ Rt, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t row0, int64_t nr,
+        int L0, int L1, int NL, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * RS_WPB + (threadIdx.x >> 6);
+  if (r >= nr) return;                        // whole waves
+  const int64_t row = row0 + r, f = row / D, s = row % D;
+  const uint64_t* k = keys + r * A;
+  const uint16_t* ix = idx + r * A;
+  uint32_t* Ps = scratch + r * A;
+  int64_t lo = 0, hi = A;                     // nv = first sentinel position
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (k[m] == KEY_SENTINEL) hi = m; else lo = m + 1;
+  }
+  const int64_t nv = lo;
+  const uint64_t below = (1ull << lane) - 1ull;        // lanes < mine
+  const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  for (int m = 0; m < NL; ++m) {
+    const int64_t t = s + (m == 0 ? L0 : L1);
+    if (t >= D) continue;                     // wave-uniform
+    const double* rr = Rt + t * ld;
+    // pass 1
+    int64_t cnt = 0, carry_ps = 0;
+    bool ref = false;
+    double ax = 0.0, ar = 0.0;
+    for (int64_t q0 = 0; q0 < nv; q0 += 64) {
+      const int64_t q = q0 + lane;
+      const bool in = q < nv;
+      const uint64_t kq = in ? k[q] : KEY_SENTINEL;
+      const uint64_t kp = (in && q > 0) ? k[q - 1] : KEY_SENTINEL;
+      const double rv = in ? rr[ix[q]] : qnan();
+      const bool pv = in && rv == rv;
+      const bool start = in && (q == 0 || kq != kp);
+      const uint64_t bs = __ballot(start), bp = __ballot(pv);
+      const int64_t Pq = cnt + __popcll(bp & below);
+      const uint64_t mine = bs & incl;
+      const int sl = mine ? 63 - __builtin_clzll(mine) : 0;
+      const int64_t sh = __shfl(Pq, sl, 64);
+      if (in) Ps[q] = (uint32_t)(mine ? sh : carry_ps);
+      if (bs) carry_ps = __shfl(Pq, 63 - __builtin_clzll(bs), 64);
+      if (!ref && bp) {
+        const int l = __ffsll((unsigned long long)bp) - 1;
+        ax = __shfl(okey_inv(kq), l, 64);
+        ar = __shfl(rv, l, 64);
+        ref = true;
+      }
+      cnt += __popcll(bp);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // pass 2
+    const int64_t tot = cnt;
+    double sm[6] = {0, 0, 0, 0, 0, 0};
+    double kk = 0.0;
+    uint32_t dif = 0;
+    int64_t carry_pe = tot, suf = 0;          // suf: pairs at positions >= the current chunk end
+    if (tot >= 3) {
+      for (int64_t q0 = ((nv - 1) / 64) * 64; q0 >= 0; q0 -= 64) {
+        const int64_t q = q0 + lane;
+        const bool in = q < nv;
+        const uint64_t kq = in ? k[q] : KEY_SENTINEL;
+        const uint64_t kp = (in && q > 0) ? k[q - 1] : KEY_SENTINEL;
+        const double rv = in ? rr[ix[q]] : qnan();
+        const bool pv = in && rv == rv;
+        const bool start = in && (q == 0 || kq != kp);
+        const uint64_t bs = __ballot(start), bp = __ballot(pv);
+        const int64_t Pq = tot - (suf + __popcll(bp & ~below));     // pairs before q
+        const uint64_t above = bs & ~incl;                          // run starts after my lane
+        const int el = above ? __builtin_ctzll(above) : 0;
+        const int64_t eh = __shfl(Pq, el, 64);
+        const int64_t Pe = above ? eh : carry_pe;
+        if (bs) carry_pe = __shfl(Pq, __builtin_ctzll(bs), 64);
+        suf += __popcll(bp);
+        if (pv) {
+          const double x = okey_inv(kq);
+          const double k2 = (double)((int64_t)Ps[q] + Pe + 1);
+          const double dx = x - ax, dy = rv - ar;
+          dif |= ((x != ax) ? 1u : 0u) | ((rv != ar) ? 2u : 0u);
+          sm[0] += dx; sm[1] += dy;
+          sm[2] += dx * dx; sm[3] += dy * dy; sm[4] += dx * dy;
+          sm[5] += k2 * dy;
+          kk += k2 * k2;                      // exact: < 2^53
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) sm[q] = rs_wsum(sm[q]);
+    kk = rs_wsum(kk);
+    const bool xvar = __ballot(dif & 1u) != 0, rvar = __ballot(dif & 2u) != 0;
+    if (lane == 0) {
+      double* o = out + ((int64_t)(m * 4) * F + f) * D + t;
+      const int64_t stp = F * D;
+      const double nn = (double)tot;
+      double ic = qnan(), ric = qnan(), beta = qnan();
+      if (tot >= 3) {
+        const double sx = sm[0], sy = sm[1];
+        if (xvar && rvar) {
+          const double sxy = sm[4] - sx * sy / nn;
+          const double sxx = sm[2] - sx * sx / nn;
+          const double syy = sm[3] - sy * sy / nn;
+          const double skk = kk / 4.0 - nn * (nn + 1.0) * (nn + 1.0) / 4.0;
+          const double sky = 0.5 * sm[5] - 0.5 * (nn + 1.0) * sy;
+          ic = fmin(1.0, fmax(-1.0, sxy / sqrt(sxx * syy)));
+          ric = fmin(1.0, fmax(-1.0, sky / sqrt(skk * syy)));
+        }
+        const double sxx_raw = sm[2] + 2.0 * ax * sx + nn * ax * ax;
+        const double sxr_raw = sm[4] + ax * sy + ar * sx + nn * ax * ar;
+        beta = sxx_raw > 0 ? sxr_raw / sxx_raw : qnan();
+      }
+      o[0] = nn;
+      o[stp] = ic;
+      o[2 * stp] = ric;
+      o[3 * stp] = beta;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// dates t < L get an empty record (n = 0, NaN stats)
+__global__ void k_rs_ic_empty(double* out, int64_t F, int64_t D, int L, int m) {
+  const int64_t f = blockIdx.x;
+  for (int64_t td = threadIdx.x; td < min<int64_t>(L, D); td += blockDim.x) {
+    double* o = out + ((int64_t)(m * 4) * F + f) * D + td;
+    o[0] = 0.0;
+    o[F * D] = qnan();
+    o[2 * F * D] = qnan();
+    o[3 * F * D] = qnan();
+  }
+}
+
 static int64_t rs_chunk_rows(int64_t rows, int64_t A) {
   return std::max<int64_t>(1, std::min<int64_t>({rows, RS_CHUNK_ELEMS / std::max<int64_t>(A, 1), (int64_t)65535}));
 }
@@ -423,6 +575,48 @@ extern "C" fmx_status fmx_cs_quantile_sorted(int32_t op, const double* X, double
 extern "C" int64_t fmx_group_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A) {
   if (F <= 0 || D <= 0 || A <= 0) return 0;
   return rs_work_bytes(F * D, A, true);
+}
+
+extern "C" int64_t fmx_ic_daily_sorted_work_bytes(int64_t F, int64_t D, int64_t A) {
+  if (F <= 0 || D <= 0 || A <= 0) return 0;
+  return rs_work_bytes(F * D, A, false);
+}
+
+extern "C" fmx_status fmx_ic_daily_sorted(const double* X, const double* R, int64_t F, int64_t D, int64_t A,
+                                          int64_t ld, const int32_t* lags, int32_t n_lags, double* out, void* work,
+                                          int64_t work_bytes, void* stream) {
+  FMX_ARG(X && R && out && lags, "null pointer");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims (A <= 65535)");
+  FMX_ARG(n_lags >= 1 && n_lags <= 8, "n_lags");
+  for (int i = 0; i < n_lags; ++i) FMX_ARG(lags[i] >= 0, "lags must be >= 0");
+  if (F == 0 || D == 0) return FMX_OK;
+  if (!work || work_bytes < fmx_ic_daily_sorted_work_bytes(F, D, std::max<int64_t>(A, 1))) {
+    set_error("workspace smaller than fmx_ic_daily_sorted_work_bytes()");
+    return FMX_ERR_ARG;
+  }
+  hipStream_t st = as_stream(stream);
+  for (int m = 0; m < n_lags; ++m) {
+    k_rs_ic_empty<<<(unsigned)F, 64, 0, st>>>(out, F, D, lags[m], m);
+    FMX_LAUNCH_CHECK("k_rs_ic_empty");
+  }
+  if (A == 0) return FMX_OK;
+  const int64_t rows = F * D, cr = rs_chunk_rows(rows, A);
+  RsWork w = rs_carve(work, rows, A, false);
+  for (int64_t r0 = 0; r0 < rows; r0 += cr) {
+    const int64_t nr = std::min(cr, rows - r0);
+    fmx_status e = rs_sort_chunk(X, nullptr, D, A, ld, r0, nr, w, st);
+    if (e) return e;
+    uint32_t* scr = reinterpret_cast<uint32_t*>(w.kin);     // the sort's input keys are dead
+    for (int base = 0; base < n_lags; base += 2) {
+      const int NL = std::min(2, n_lags - base);
+      const int L0 = lags[base], L1 = NL > 1 ? lags[base + 1] : 0;
+      double* o = out + (int64_t)base * 4 * F * D;
+      k_rs_ic<<<(unsigned)ceil_div(nr, RS_WPB), 64 * RS_WPB, 0, st>>>(w.kout, w.vout, scr, R, F, D, A, ld, r0, nr,
+                                                                     L0, L1, NL, o);
+      FMX_LAUNCH_CHECK("k_rs_ic");
+    }
+  }
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_group_rank_sorted(const double* X, const int32_t* G, double* Y, int64_t F, int64_t D,

@@ -22,11 +22,14 @@ namespace fmx {
 
 constexpr int SIM_BLOCK = 256;
 
+// STAGED: the row lives in LDS (A <= 20,480); else every pass re-reads it from HBM / L2
+// (the cell value, masked by presence, is recomputed on the fly) -- any row length.
+template <bool STAGED>
 __global__ void __launch_bounds__(SIM_BLOCK)
 k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
               double* __restrict__ Wshift, double* __restrict__ counts, int64_t D, int64_t A, double pct,
               int nan_absent) {
-  extern __shared__ double sx[];  // [A]
+  extern __shared__ double sx[];  // [A] (STAGED)
   __shared__ int s_npos, s_nneg, s_npres;
   __shared__ unsigned s_hist[512];
   __shared__ uint64_t s_prefix[2], s_mask[2];
@@ -40,6 +43,11 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   const double* x = X + d * A;
   const uint8_t* p = present ? present + d * A : nullptr;
   double* w = W + d * A;
+  auto cell = [&](int64_t a) {
+    if (STAGED) return sx[a];
+    const double xv = x[a];
+    return ((!p || p[a]) && (!nan_absent || xv == xv)) ? xv : __builtin_nan("");
+  };
   if (threadIdx.x == 0) { s_npos = 0; s_nneg = 0; s_npres = 0; }
   __syncthreads();
   int np = 0, nn = 0, npr = 0;
@@ -48,7 +56,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
     const bool pr = (!p || p[a]) && (!nan_absent || x[a] == x[a]);
     npr += pr;
     const double v = pr ? x[a] : __builtin_nan("");
-    sx[a] = v;
+    if (STAGED) sx[a] = v;
     np += v > 0.0;
     nn += v < 0.0;
   }
@@ -82,7 +90,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
       __syncthreads();
       const uint64_t m0 = s_mask[0], m1 = s_mask[1], p0 = s_prefix[0], p1 = s_prefix[1];
       for (int64_t a = threadIdx.x; a < A; a += SIM_BLOCK) {
-        const double v = sx[a];
+        const double v = cell(a);
         if (v > 0.0) {
           const uint64_t k = (uint64_t)__double_as_longlong(v);
           if ((k & m0) == p0) atomicAdd(&s_hist[(k >> shift) & 255], 1u);
@@ -136,7 +144,7 @@ k_trade_equal(const double* __restrict__ X, const uint8_t* __restrict__ present,
   for (int64_t a0 = 0; a0 < A; a0 += SIM_BLOCK) {
     const int64_t a = a0 + threadIdx.x;
     const bool in = a < A;
-    const double v = in ? sx[a] : __builtin_nan("");
+    const double v = in ? cell(a) : __builtin_nan("");
     const bool lg = v > 0.0;
     const uint64_t k = (uint64_t)__double_as_longlong(lg ? v : -v);
     const bool tie0 = !flat && lg && k == t0, tie1 = !flat && v < 0.0 && k == t1;
@@ -410,6 +418,119 @@ k_trade_linear(const double* __restrict__ X, const uint8_t* __restrict__ present
   }
 }
 
+// Trade list 'linear' on rows past 16,384 assets (k_trade_linear holds a row in registers):
+// the same operations in the same order, with the row's weights held in its output row W
+// (not registers) and each subset compacted, in asset order, into Wsub's row (the shifted
+// book, written by k_shift_rows afterwards) instead of LDS.  One workgroup per (date,
+// manager).  ful / fus are read off the capped weight c: for mw > 0, w > 0 && c < mw <=>
+// 0 < c < mw (and w < 0 && c > -mw <=> -mw < c < 0).
+__global__ void __launch_bounds__(LIN_NT)
+k_trade_linear_xl(const double* __restrict__ X, const uint8_t* __restrict__ present, double* __restrict__ W,
+                  double* __restrict__ Wsub, double* __restrict__ counts, int64_t D, int64_t A, double mw, PwTable pw,
+                  int nan_absent) {
+  __shared__ double nodes[2 * (65536 / 64) + 8];
+  __shared__ int iscr[LIN_NW + 2];
+  const int t = threadIdx.x;
+  const int64_t d = blockIdx.x, mgr = blockIdx.y;
+  const double* x = X + mgr * D * A + d * A;
+  const uint8_t* p = present ? present + d * A : nullptr;
+  double* w = W + mgr * D * A + d * A;
+  double* sub = Wsub + mgr * D * A + d * A;
+  counts += mgr * D * 2;
+  auto pres = [&](int64_t a) {
+    const double xv = x[a];
+    return (!p || p[a]) && (!nan_absent || xv == xv);
+  };
+  int c3[3] = {0, 0, 0};
+  for (int64_t a = t; a < A; a += LIN_NT) {
+    const bool pr = pres(a);
+    const double v = pr ? x[a] : 0.0;
+    c3[0] += pr;
+    c3[1] += pr && v > 0.0;
+    c3[2] += pr && v < 0.0;
+    w[a] = (pr && (v > 0.0 || v < 0.0)) ? v : 0.0;   // weights[pos.index] = pos, [neg.index] = neg
+  }
+  int tot[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    block_exscan<LIN_NT>(c3[i], iscr, &tot[i]);
+    __syncthreads();
+  }
+  const int npos = tot[1], nneg = tot[2];
+  const bool anyrow = tot[0] > 0;
+  const bool flat = npos == 0 || nneg == 0;
+  // numpy pairwise sum over the cells a < A with sel(a), of val(a), in asset order
+  auto csum = [&](auto val, auto sel) {
+    int m = 0;
+    for (int64_t c0 = 0; c0 < A; c0 += LIN_NT) {
+      const int64_t a = c0 + t;
+      const bool in = a < A && sel(a);
+      int n;
+      const int off = block_exscan<LIN_NT>(in ? 1 : 0, iscr, &n);
+      if (in) sub[m + off] = val(a);
+      m += n;
+      __syncthreads();
+    }
+    int cnt;
+    return block_pw_sum_w0<LIN_NT>([&](int i) { return sub[i]; }, [](int) { return 0; }, pw.get(m), nodes, iscr,
+                                   &cnt);
+  };
+  if (!flat) {
+    // _normalize_legs: w_pos = clip(lower=0), w_neg = clip(upper=0), sums over all n rows
+    const double sp = csum([&](int64_t a) { const double v = w[a]; return v >= 0.0 ? v : 0.0; }, pres);
+    const double sn = csum([&](int64_t a) { const double v = w[a]; return v <= 0.0 ? v : 0.0; }, pres);
+    for (int64_t a = t; a < A; a += LIN_NT) {
+      const double v = w[a];
+      const double wp = v >= 0.0 ? v : 0.0, wn = v <= 0.0 ? v : 0.0;
+      const double aa = sp > 0.0 ? wp / sp : wp;
+      const double bb = sn < 0.0 ? wn / -sn : wn;
+      w[a] = aa + bb;
+    }
+    __syncthreads();
+    // _cap_and_redistribute(max_weight, max_iter=10, tol=1e-6): w becomes c in place
+    const double tol = 1e-6;
+    for (int it = 0; it < 10; ++it) {
+      bool ul = false, us = false;
+      for (int64_t a = t; a < A; a += LIN_NT) {
+        double v = w[a] >= -mw ? w[a] : -mw;
+        v = v <= mw ? v : mw;
+        w[a] = v;
+        const bool pr = pres(a);
+        ul |= pr && v > 0.0 && v < mw;
+        us |= pr && v < 0.0 && v > -mw;
+      }
+      __syncthreads();
+      const double le = 1.0 - csum([&](int64_t a) { return w[a]; }, [&](int64_t a) { return pres(a) && w[a] > 0.0; });
+      const double se = -1.0 - csum([&](int64_t a) { return w[a]; }, [&](int64_t a) { return pres(a) && w[a] < 0.0; });
+      const bool any_ul = __syncthreads_or(ul), any_us = __syncthreads_or(us);
+      if ((fabs(le) < tol && fabs(se) < tol) || (!any_ul && !any_us)) break;
+      auto ful = [&](int64_t a) { const double v = w[a]; return pres(a) && v > 0.0 && v < mw; };
+      auto fus = [&](int64_t a) { const double v = w[a]; return pres(a) && v < 0.0 && v > -mw; };
+      if (any_ul && fabs(le) > tol) {
+        const double su = csum([&](int64_t a) { return w[a]; }, ful);
+        for (int64_t a = t; a < A; a += LIN_NT)
+          if (ful(a)) w[a] = w[a] + le * (w[a] / su);
+        __syncthreads();
+      }
+      if (any_us && fabs(se) > tol) {
+        const double su = csum([&](int64_t a) { return w[a]; }, fus);
+        for (int64_t a = t; a < A; a += LIN_NT)
+          if (fus(a)) w[a] = w[a] + se * (w[a] / su);
+        __syncthreads();
+      }
+    }
+  }
+  for (int64_t a = t; a < A; a += LIN_NT) {
+    double v = w[a] >= -mw ? w[a] : -mw;
+    v = v <= mw ? v : mw;
+    w[a] = pres(a) ? (flat ? 0.0 : v) : __builtin_nan("");
+  }
+  if (t == 0) {                                   // counts (len(pos), len(neg)); NaN: no rows
+    counts[2 * d] = anyrow ? (flat ? 0.0 : (double)npos) : __builtin_nan("");
+    counts[2 * d + 1] = anyrow ? (flat ? 0.0 : (double)nneg) : __builtin_nan("");
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Simulation._daily_portfolio_returns (portfolio_simulation.py:748-797)
 // on the aligned [D][A] grid (union of the weights' and returns' dates and symbols; NaN =
@@ -578,21 +699,34 @@ extern "C" fmx_status fmx_daily_corr(const double* X, const double* R, double* o
 static fmx_status trade_book(int method, const double* X, const uint8_t* present, int nan_absent, double* Wraw,
                              double* Wout, double* counts, int64_t F, int64_t D, int64_t A, double pct, double mw,
                              hipStream_t st) {
-  FMX_ARG(X && Wraw && Wout && counts && F >= 0 && D >= 0 && A >= 0, "bad args");
+  FMX_ARG(X && Wraw && Wout && counts && F >= 0 && D >= 0 && A >= 0 && A <= (1 << 20), "bad args");
   FMX_ARG(Wraw != Wout && Wraw != X, "Wraw must not alias X or Wout");
-  FMX_ARG(A <= 16384, "trade list holds one date row per workgroup: A <= 16384");
   FMX_ARG(pct >= 0.0, "pct must be >= 0");
   FMX_ARG(F <= 65535 && D <= 0x7fffffffll, "too many managers / dates");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
-  const bool ragged = present || nan_absent;
+  // rows past 16,384 assets: the linear book keeps its row in HBM (k_trade_linear_xl uses
+  // Wout's row as scratch), then the shift runs as on a ragged panel
+  const bool xl = A > 16384;
+  FMX_ARG(!xl || method == 0 || mw > 0.0, "rows past 16384 assets: max_weight must be > 0 for 'linear'");
+  const bool ragged = present || nan_absent || (xl && method == 1);
   double* ws = ragged ? nullptr : Wout;             // dense: the kernel writes the shifted book
   const size_t lds = (size_t)A * sizeof(double);
   if (method == 0) {
-    if (lds > 64 * 1024)
-      FMX_HIP(hipFuncSetAttribute((const void*)k_trade_equal, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_trade_equal<<<dim3((unsigned)D, (unsigned)F), SIM_BLOCK, lds, st>>>(X, present, Wraw, ws, counts, D, A, pct,
-                                                                           nan_absent);
-    FMX_LAUNCH_CHECK("k_trade_equal");
+    const bool staged = lds <= 160 * 1024 - 8192;
+    const void* k = staged ? (const void*)k_trade_equal<true> : (const void*)k_trade_equal<false>;
+    const size_t dl = staged ? lds : 0;
+    if (dl > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl));
+    void* args[] = {(void*)&X, (void*)&present, (void*)&Wraw, (void*)&ws, (void*)&counts, (void*)&D, (void*)&A,
+                    (void*)&pct, (void*)&nan_absent};
+    FMX_HIP(hipLaunchKernel(k, dim3((unsigned)D, (unsigned)F), dim3(SIM_BLOCK), args, dl, st));
+  } else if (xl) {
+    fmx_status e = FMX_OK;
+    PwTable pw = pw_table((int)A, &e);
+    if (e) return e;
+    void* args[] = {(void*)&X, (void*)&present, (void*)&Wraw, (void*)&Wout, (void*)&counts, (void*)&D, (void*)&A,
+                    (void*)&mw, (void*)&pw, (void*)&nan_absent};
+    FMX_HIP(hipLaunchKernel((const void*)k_trade_linear_xl, dim3((unsigned)D, (unsigned)F), dim3(LIN_NT), args, 0,
+                            st));
   } else {
     fmx_status e = FMX_OK;
     PwTable pw = pw_table((int)A, &e);

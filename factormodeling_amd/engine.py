@@ -292,7 +292,10 @@ def cs_quantile_op(kind: str, X, qlo: float, qhi: float, present=None, out=None)
     return Y
 
 
-def group_op(op: str, X, G, ngroups: int, method="average", present=None):
+def group_op(op: str, X, G, ngroups: int, method="average", present=None, long_rows=None):
+    """Group ops (operations.py:104-168).  Rows past 16,384 assets (or ``long_rows=True``):
+    rank from rows sorted by (group, value) in HBM, mean / neutralize / normalize with the
+    members compacted in HBM scratch (fmx_group_op_long)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
@@ -318,8 +321,13 @@ def group_op(op: str, X, G, ngroups: int, method="average", present=None):
             call("fmx_group_rank_sorted", ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method],
                  ptr(present), ptr(work), wb, stream_ptr())
             return Y
-    elif A > FINE_RANK_MAX_A:
-        raise _lib.FmxError(f"group_{op} on rows of more than {FINE_RANK_MAX_A} assets is not supported")
+    elif op != "rank" and (long_rows or (long_rows is None and A > FINE_RANK_MAX_A)):
+        Y = torch.empty_like(X)
+        nb = int(_lib.load().fmx_group_op_long_work_bytes(F, D, A))
+        work, wb = _workspace_bytes(X.device, nb)
+        call("fmx_group_op_long", GROUP[op], ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), ptr(present),
+             ptr(work), wb, stream_ptr())
+        return Y
     Y = torch.empty_like(X)
     call("fmx_group_op", GROUP[op], ptr(X), ptr(G), ptr(Y), F, D, A, A, int(ngroups), RANK[method], ptr(present),
          stream_ptr())
@@ -352,10 +360,11 @@ def bucket_codes(X, edges: np.ndarray):
 
 
 # ----------------------------------------------------------------------------- IC / selection
-def ic_daily(X, R, lags=(1,), rank2=None):
+def ic_daily(X, R, lags=(1,), rank2=None, sorted_rows=None):
     """[n_lags][4][F][D] = (n_pairs, IC, rank_IC, beta) for pairs (X[f][t-L], R[t]).
     ``rank2``: the doubled ranks of X from ``cs_rank_winsor(X, rank2=...)`` -- the rows
-    are then not ranked again (fmx_ic_daily_ranked, identical records)."""
+    are then not ranked again (fmx_ic_daily_ranked, identical records).  Rows past 16,384
+    assets (or ``sorted_rows=True``) are sorted in HBM (fmx_ic_daily_sorted)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
@@ -370,6 +379,13 @@ def ic_daily(X, R, lags=(1,), rank2=None):
         work = _workspace(X.device, n)
         call("fmx_ic_daily_ranked", ptr(X), ptr(rank2), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p),
              len(lags), ptr(work), n, ptr(out), stream_ptr())
+        return out
+    if sorted_rows or (sorted_rows is None and A > RANKED_IC_MAX_A):
+        # rows past the fine / LDS kernels: sorted in HBM, ranks read off the sorted rows
+        nb = int(_lib.load().fmx_ic_daily_sorted_work_bytes(F, D, A))
+        work, wb = _workspace_bytes(X.device, nb)
+        call("fmx_ic_daily_sorted", ptr(X), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p), len(lags),
+             ptr(out), ptr(work), wb, stream_ptr())
         return out
     call("fmx_ic_daily", ptr(X), ptr(R), F, D, A, A, ctypes.cast(lag_h, ctypes.c_void_p), len(lags), ptr(out),
          stream_ptr())

@@ -203,6 +203,15 @@ fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D
  * average / min / max / first / dense. */
 fmx_status fmx_group_op(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F, int64_t D, int64_t A,
                         int64_t ld, int32_t ngroups, int32_t method, const uint8_t* present, void* stream);
+/* group_mean / group_neutralize / group_normalize (operations.py:112-149) on rows of ANY
+ * length up to 65,535 assets (fmx_group_op holds a row in registers: A <= 16384): rows
+ * stay in HBM, each group's members are compacted in asset order into device scratch and
+ * summed with numpy's pairwise schedule (bit-identical to fmx_group_op where both run).
+ * Codes outside [0, ngroups) = no group.  work: fmx_group_op_long_work_bytes(F, D, A). */
+int64_t fmx_group_op_long_work_bytes(int64_t F, int64_t D, int64_t A);
+fmx_status fmx_group_op_long(int32_t op, const double* X, const int32_t* G, double* Y, int64_t F, int64_t D, int64_t A,
+                             int64_t ld, int32_t ngroups, const uint8_t* present, void* work, int64_t work_bytes,
+                             void* stream);
 /* cs_regression (operations.py:248-304) for one [D][ld] pair. */
 fmx_status fmx_cs_regression(const double* Yv, const double* Xv, double* Out, int64_t D, int64_t A, int64_t ld,
                              int32_t rettype, const uint8_t* present, void* stream);
@@ -218,6 +227,16 @@ fmx_status fmx_bucket(const double* X, int32_t* codes, int64_t n, const double* 
  * undefined.  Each exposure row is ranked once for up to two lags. */
 fmx_status fmx_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                         const int32_t* lags, int32_t n_lags, double* out, void* stream);
+/* Daily IC records for rows of ANY length up to 65,535 assets (the fine kernels' 16-bit
+ * doubled ranks end at 16,384; factor_selector.py:36-48 has no limit): each (f, s) row
+ * is sorted in HBM (rocPRIM segmented radix sort, chunks of rows), then one wave per row
+ * ranks each lag's pair-valid subset off the sorted keys and reduces the same
+ * (n, IC, rank IC, beta) records as fmx_ic_daily (out layout identical).  work:
+ * fmx_ic_daily_sorted_work_bytes(F, D, A) bytes of device scratch. */
+int64_t fmx_ic_daily_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
+fmx_status fmx_ic_daily_sorted(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
+                               const int32_t* lags, int32_t n_lags, double* out, void* work, int64_t work_bytes,
+                               void* stream);
 /* fmx_ic_daily for a panel whose rows fmx_cs_rank_winsor already ranked (rank2): the
  * rank among each lag's pairs is rank2 corrected by the exposures whose return is NaN, so
  * no row is ranked again; one wavefront per row (single-pass shifted moments: records

@@ -124,3 +124,123 @@ def test_group_rank_big_groups(dev, A, big, method):
                      method).cpu().numpy()[0]
     ref = O.group_rank_normalized(x, g, method=method)
     assert_close(got.ravel(), ref.ravel(), exact=True, what=f"group rank {method} A={A}")
+
+
+def _ic_case(seed, F, D, A):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.02] = np.nan
+    X = np.where(rng.random(X.shape) < 0.3, np.round(X, 1), X)        # heavy ties
+    X[1, 2] = 0.75                                                   # a constant row: IC NaN
+    X[0, 3, 3:] = np.nan                                             # < 3 pairs
+    R = 0.01 * rng.standard_normal((D, A)) + 0.002 * np.nan_to_num(X[0])
+    R[rng.random(R.shape) < 0.03] = np.nan
+    R[4] = np.nan                                                    # a date with no returns
+    return X, R
+
+
+def test_ic_daily_20000_assets(dev):
+    """the daily IC (factor_selector.py:36-48) past 16,384 assets, from
+    rows sorted in HBM (fmx_ic_daily_sorted) vs the oracle's scipy restatement."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.metrics as OM
+    F, D, A = 3, 7, 20000
+    X, R = _ic_case(29, F, D, A)
+    out = E.ic_daily(torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev), (1, 2)).cpu().numpy()
+    for li, L in enumerate((1, 2)):
+        for f in range(F):
+            for t in range(D):
+                if t < L:
+                    assert out[li, 0, f, t] == 0 and np.isnan(out[li, 1:, f, t]).all()
+                    continue
+                n, ic, ric, beta = OM.daily_stats(X[f, t - L], R[t])
+                assert out[li, 0, f, t] == n
+                assert_close(out[li, 1:, f, t], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12,
+                             what=f"{L},{f},{t}")
+
+
+def test_ic_sorted_rows_match_wave_kernels_on_short_rows(dev):
+    """The sorted-row IC and the fine / wave kernels (pinned to the reference's goldens)
+    give the same records on short rows: counts exact, statistics to 1e-12."""
+    import torch
+    import factormodeling_amd.engine as E
+    X, R = _ic_case(31, 4, 9, 700)
+    Xd, Rd = torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev)
+    a = E.ic_daily(Xd, Rd, (1, 2), sorted_rows=True).cpu().numpy()
+    b = E.ic_daily(Xd, Rd, (1, 2), sorted_rows=False).cpu().numpy()
+    assert np.array_equal(a[:, 0], b[:, 0])
+    assert_close(a[:, 1:].ravel(), b[:, 1:].ravel(), rtol=1e-12, atol=1e-14, what="sorted vs wave IC")
+
+
+@pytest.mark.parametrize("op", ["mean", "neutralize", "normalize"])
+@pytest.mark.parametrize("A,ragged", [(20000, False), (20000, True), (700, False)])
+def test_group_moments_long_rows(dev, op, A, ragged):
+    """group_mean / group_neutralize / group_normalize past 16,384
+    assets (fmx_group_op_long: members compacted in HBM scratch, numpy pairwise sums), bit-
+    exact vs the oracle; on a short row the long-row kernel equals fmx_group_op bit for bit."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.ops as O
+    rng = np.random.default_rng(A + len(op) + ragged)
+    D = 3
+    x = _rows(A + 1, D, A, nan=0.03)
+    g = rng.integers(0, 11, size=(D, A)).astype(np.float64)
+    g[rng.random(g.shape) < 0.01] = np.nan
+    g[1, :] = np.where(np.isnan(g[1]), np.nan, 3.0)                  # one group holds the whole row
+    x[2, g[2] == 6.0] = 0.25                                          # a constant group: sigma 0 -> 0
+    codes = np.where(np.isnan(g), -1, g).astype(np.int32)
+    p = None
+    if ragged:
+        p = np.random.default_rng(5).random((D, A)) > 0.2
+    pt = None if p is None else torch.as_tensor(p.astype(np.uint8), device=dev)
+    xt, gt = torch.as_tensor(x[None], device=dev), torch.as_tensor(codes, device=dev)
+    got = E.group_op(op, xt, gt, 11, present=pt, long_rows=True).cpu().numpy()[0]
+    ref = getattr(O, "group_" + op)(x, g, p)
+    assert_close(got.ravel(), ref.ravel(), exact=True, what=f"group_{op} A={A}")
+    if A <= 16384:
+        short = E.group_op(op, xt, gt, 11, present=pt, long_rows=False).cpu().numpy()[0]
+        assert np.array_equal(got, short, equal_nan=True)
+
+
+@pytest.mark.parametrize("A,ragged", [(20000, False), (20000, True), (26000, False)])
+def test_trade_equal_long_rows(dev, A, ragged):
+    """Trade list 'equal' past 16,384 assets (LDS-staged row up to ~19,400, re-read from
+    HBM beyond) vs the oracle, bit-exact."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.simulation as OS
+    rng = np.random.default_rng(A)
+    D = 5
+    X = rng.standard_normal((D, A))
+    X[rng.random(X.shape) < 0.02] = np.nan
+    X[2] = np.abs(X[2])                                               # flat day
+    X[3] = rng.integers(-2, 3, A).astype(np.float64)                  # tie blocks at the k-th value
+    present = rng.random((D, A)) >= 0.1 if ragged else np.ones((D, A), dtype=bool)
+    pres = torch.as_tensor(present.astype(np.uint8), device=dev) if ragged else None
+    got, c = E.trade_equal(torch.as_tensor(X, device=dev), 0.1, present=pres)
+    want, wc = OS.trade_equal(X, present, 0.1)
+    assert np.array_equal(got.cpu().numpy(), want, equal_nan=True)
+    np.testing.assert_array_equal(c.cpu().numpy(), wc)
+
+
+@pytest.mark.parametrize("A,ragged", [(20000, False), (20000, True)])
+def test_trade_linear_long_rows(dev, A, ragged):
+    """Trade list 'linear' (normalised legs + cap-and-redistribute) past 16,384 assets
+    (k_trade_linear_xl: the row in HBM) vs the oracle's numpy-pairwise restatement, bit-exact."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.simulation as OS
+    rng = np.random.default_rng(A + 1)
+    D = 4
+    X = rng.standard_normal((D, A))
+    X[rng.random(X.shape) < 0.02] = np.nan
+    X[1] = np.abs(X[1])                                               # flat day
+    X[2, :40] = 50.0                                                  # a few huge signals: capped
+    present = rng.random((D, A)) >= 0.1 if ragged else np.ones((D, A), dtype=bool)
+    pres = torch.as_tensor(present.astype(np.uint8), device=dev) if ragged else None
+    mw = 0.0005
+    got, c = E.trade_linear(torch.as_tensor(X, device=dev), mw, present=pres)
+    want, wc = OS.trade_linear(X, present, mw)
+    assert np.array_equal(got.cpu().numpy(), want, equal_nan=True)
+    np.testing.assert_array_equal(c.cpu().numpy(), wc)

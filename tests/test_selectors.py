@@ -59,7 +59,8 @@ def test_icir_top_and_momentum_match_reference_formulation(seed):
 
 def test_mvo_selector_needs_the_reference_checkout(monkeypatch):
     monkeypatch.delenv("FMX_REFERENCE_DIR", raising=False)
-    monkeypatch.setattr(M, "_REF_FSM", None)
+    import factormodeling_amd._refload as RL
+    monkeypatch.setattr(RL, "_CACHE", {})
     df = pd.DataFrame({"IC_IR": [0.1], "rank_IC_IR": [0.1]}, index=["a"])
     with pytest.raises(NotImplementedError, match="FMX_REFERENCE_DIR"):
         M.mvo_selector(df, None, None, pd.DataFrame({"a": [0.01]}), "t", 1)
