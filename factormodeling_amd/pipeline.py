@@ -460,8 +460,9 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
             be.op(kind, op, w, X, outs[0])
     _rec(timers, name, t0)
     if collect is not None:
+        fs = collect.get("_factors")             # full-size tests: only a sample of factors
         for o, y in zip(ops, outs):
-            collect[_op_key(*o)] = y[:, own].clone()
+            collect[_op_key(*o)] = (y if fs is None else y[fs])[:, own].clone()
 
 
 def _fused_ic(be, side):
@@ -514,14 +515,15 @@ def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
             else:
                 be.op("ts", op, w, Xc, out)
             _rec(timers, f"ret:{'corr' if op == 'corr_vol' else op}:{w}", t0)
-            if collect is not None:
+            if collect is not None and collect.get("_factors") is None:
                 collect.setdefault(f"ret:{'corr' if op == 'corr_vol' else op}:{w}", []).append(out[:, sp.halo:].clone())
             if op == "corr_vol":
                 t0 = _ev(timers)
                 be.corr_vol_feature(Xc, out, w, sp.feature[f0:f1])
                 _rec(timers, f"ret:cvf:{w}", t0)
     if collect is not None and getattr(sp, "feature", None) is not None:
-        collect["feature"] = sp.feature[:, sp.halo:].clone()
+        fs = collect.get("_factors")
+        collect["feature"] = (sp.feature if fs is None else sp.feature[fs])[:, sp.halo:].clone()
 
 
 def _step_panel(sp, cfg):

@@ -14,6 +14,7 @@ if HERE not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: larger CPU test")
+    config.addinivalue_line("markers", "fullsize: a benchmark config at full size on the GPU (minutes, ~250 GB HBM)")
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,198 @@
+"""Full-size checks of the benchmark configs on one MI355X (BASELINE
+configs[1], [3], [4]): the shape-dependent planning (the wide Gram's date blocks, the rank
+kernels' row tiling, the IC's chunking, C5's factor chunks) runs at the sizes it is timed
+at, and sampled outputs are checked against the oracle / plain fp64 recomputation.
+
+* C2 (2520 x 5000 x 200): the whole step; 4 sampled factors' nine operator outputs
+  bit-exact (decay <= 1e-12 rel) vs the oracle, their daily IC (both lags) on sampled
+  dates vs the oracle's scipy restatement (<= 1e-9), the selection of sampled days
+  recomputed from the step's window metrics (bit-exact sets), 64 sampled C entries vs a
+  plain fp64 recomputation (<= 1e-10), and the kept set vs a host greedy walk of C.
+* C4 (2520 x 3000 x 2000): the wide exact Gram; C symmetric with a unit diagonal on valid
+  rows, 64 sampled entries + their pair counts vs plain fp64 / integer recomputation.
+* C5 (2520 x 10000 x 500): 2 sampled factors' feature panel sign(ts_corr) * x / ts_std
+  bit-exact vs the oracle, and their daily IC on sampled dates.
+
+Each test frees its device memory before the next (C5 alone uses ~250 GB of HBM).
+"""
+import gc
+
+import numpy as np
+import pytest
+
+from golden_io import assert_close
+
+pytestmark = [pytest.mark.gpu, pytest.mark.fullsize]
+
+
+@pytest.fixture
+def dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    yield torch.device("cuda", 0)
+    import factormodeling_amd.engine as E
+    E._WORK.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def _zgram(Xf, Xg):
+    """Plain fp64 z-score Gram entry of two [D][A] device rows (ddof 0; NaN / sigma 0 ->
+    invalid) and its pair count."""
+    import torch
+
+    def z(x):
+        m = ~torch.isnan(x)
+        n = m.sum(1, keepdim=True)
+        mu = torch.where(m, x, 0.0).sum(1, keepdim=True) / n
+        sd = torch.sqrt(torch.where(m, (x - mu) ** 2, 0.0).sum(1, keepdim=True) / n)
+        ok = m & (sd > 0)
+        return torch.where(ok, (x - mu) / sd, 0.0), ok
+    zf, mf = z(Xf)
+    zg, mg = z(Xg)
+    return float((zf * zg).sum()), int((mf & mg).sum())
+
+
+def _greedy(C, order, rho, top):
+    """Keep f iff max |C[f, kept]| < rho (a NaN max keeps it, as np.max propagates NaN)."""
+    kept = []
+    for f in order:
+        m = np.max(np.abs(C[f, kept])) if kept else -np.inf
+        if not (m >= rho):
+            kept.append(int(f))
+            if top is not None and len(kept) >= top:
+                break
+    return kept
+
+
+def _prune_order(summ):
+    """The step's pruning order: rank_IC_IR descending, NaN last, ties by position."""
+    return np.argsort(-np.nan_to_num(summ[0, :, 3], nan=-np.inf), kind="stable")
+
+
+@pytest.mark.timeout(900)
+def test_c2_full_step_sampled_vs_oracle(dev):
+    import torch
+    import oracle.metrics as OM
+    import oracle.ops as O
+    from factormodeling_amd import pipeline as PL
+    D, A, F = 2520, 5000, 200
+    cfg = PL.workload_config("c2")
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=0, halo=cfg.halo)
+    fs = [0, 57, 123, 199]
+    col = {"_factors": fs}
+    w, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    X = sp.X[fs].cpu().numpy()
+    R = sp.R.cpu().numpy()
+    ref = {"ts:mean:20": lambda x: O.ts_mean(x, 20), "ts:std:20": lambda x: O.ts_std(x, 20),
+           "ts:zscore:20": lambda x: O.ts_zscore(x, 20), "ts:rank:10": lambda x: O.ts_rank(x, 10),
+           "ts:decay:20": lambda x: O.ts_decay(x, 20), "cs_rank::": O.cs_rank, "cs:zscore:": O.cs_zscore,
+           "winsor::": O.cs_winsor, "cs:market_neutralize:": O.market_neutralize}
+    for i in range(len(fs)):
+        for key, fn in ref.items():
+            got = col[key][i].cpu().numpy()
+            exp = fn(X[i])
+            if key == "ts:decay:20":                          # <= ~W ulps of sum k|x| / sum k
+                bound = 1e-13 * np.nan_to_num(O.ts_decay(np.abs(X[i]), 20), nan=0.0) + 1e-300
+                ok = np.isnan(got) == np.isnan(exp)
+                assert ok.all() and (np.abs(np.nan_to_num(got - exp)) <= bound).all(), f"{key} f{fs[i]}"
+            else:
+                assert_close(got.ravel(), exp.ravel(), exact=True, what=f"{key} f{fs[i]}")
+    # daily IC of the sampled factors on sampled target dates (lags 1 and 2)
+    daily = col["daily"].cpu().numpy()                       # [L][4][F][D]
+    rng = np.random.default_rng(0)
+    for li, L in enumerate(cfg.ic_lags):
+        for t in sorted(rng.choice(np.arange(L, D), 60, replace=False)):
+            for i, f in enumerate(fs):
+                n, ic, ric, beta = OM.daily_stats(X[i, t - L], R[t])
+                assert daily[li, 0, f, t] == n
+                assert_close(daily[li, 1:, f, t], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12,
+                             what=f"IC L{L} f{f} t{t}")
+    # window metrics of sampled days vs the oracle's summaries of the step's daily IC series,
+    # and each day's icir_top selection recomputed from the step's window metrics
+    win = col["win"].cpu().numpy()                           # [J][F][8]
+    W = cfg.sel_window
+    proc = np.arange(W, D - 1)
+    wn = w.cpu().numpy()
+    dl = daily[len(cfg.ic_lags) - 1]
+    for j in sorted(rng.choice(len(proc), 40, replace=False)):
+        i = proc[j]
+        for f in fs:
+            s = OM.summarize(dl[1, f, i - W + 1:i], dl[2, f, i - W + 1:i], dl[3, f, i - W + 1:i])
+            assert_close(win[j, f, :7], np.asarray(s, dtype=np.float64)[:7], rtol=1e-9, atol=1e-12,
+                         what=f"window metrics day {i} f{f}")
+        order = OM.nargsort_desc(win[j, :, 3])
+        wo = OM.icir_top(order, win[j], cfg.icir_threshold, cfg.top_x)
+        wf = np.zeros(F)
+        wf[order] = wo
+        assert np.array_equal(wf, wn[j]), f"selection day {i}"
+    # correlation Gram: 64 sampled entries vs plain fp64; kept = host greedy walk of C
+    C = col["C"].cpu().numpy()
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, F, size=(64, 2))]
+    for a, b in pairs:
+        g, n = _zgram(sp.X[a], sp.X[b])
+        assert n > 0
+        np.testing.assert_allclose(C[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
+        assert C[a, b] == C[b, a]
+    assert kept == _greedy(C, _prune_order(col["summ"].cpu().numpy()), cfg.prune_rho, cfg.top_x)
+    del sp, col, w
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_wide_gram(dev):
+    import torch
+    import oracle.metrics as OM
+    from factormodeling_amd import pipeline as PL
+    D, A, F = 2520, 3000, 2000
+    cfg = PL.workload_config("c4")
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=0, halo=cfg.halo)
+    col = {"_factors": [0]}
+    _, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    C = col["C"]
+    assert torch.equal(C, C.T)
+    d = torch.diagonal(C)
+    assert float((d - 1.0).abs().max()) <= 1e-12
+    rng = np.random.default_rng(4)
+    Cn = C.cpu().numpy()
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, F, size=(64, 2))]
+    pairs += [(0, F - 1), (F - 1, F - 1), (255, 256), (1023, 1024)]     # tile / block edges
+    for a, b in pairs:
+        g, n = _zgram(sp.X[a], sp.X[b])
+        np.testing.assert_allclose(Cn[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
+    assert kept == _greedy(Cn, _prune_order(col["summ"].cpu().numpy()), cfg.prune_rho, None)
+    del sp, col, C
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_feature_sampled_vs_oracle(dev):
+    import torch
+    import oracle.metrics as OM
+    import oracle.ops as O
+    from factormodeling_amd import pipeline as PL
+    D, A, F = 2520, 10000, 500
+    cfg = PL.workload_config("c5")
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=0, halo=cfg.halo)
+    fs = [7, 431]
+    col = {"_factors": fs}
+    w, _ = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    X = sp.X[fs].cpu().numpy()
+    R = sp.R.cpu().numpy()
+    feat = col["feature"].cpu().numpy()
+    for i in range(len(fs)):
+        exp = O.corr_vol_feature(X[i], R, 60)
+        assert_close(feat[i].ravel(), exp.ravel(), exact=True, what=f"C5 feature f{fs[i]}")
+    daily = col["daily"].cpu().numpy()
+    rng = np.random.default_rng(5)
+    for li, L in enumerate(cfg.ic_lags):
+        for t in sorted(rng.choice(np.arange(60 + L, D), 20, replace=False)):
+            for i, f in enumerate(fs):
+                n, ic, ric, beta = OM.daily_stats(feat[i, t - L], R[t])
+                assert daily[li, 0, f, t] == n
+                assert_close(daily[li, 1:, f, t], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12,
+                             what=f"C5 IC L{L} f{f} t{t}")
+    assert w.shape == (D - cfg.sel_window - 1, F)
+    del sp, col, w
