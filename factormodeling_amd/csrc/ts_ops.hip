@@ -25,6 +25,21 @@
 
 namespace fmx {
 
+// RN(x / n) for an integer n >= 1 from r = RN(1 / n) (a table entry): q0 = RN(x r) is within
+// 1.5 ulp of x / n; the remainder x - q0 n is exact under an fma; q0 + r (x - q0 n) lies
+// within 1.5 * 2^-53 ulp of x / n, which is never a rounding midpoint (x / n = odd * 2^(e-1)
+// would need x to carry more than 53 bits) and sits at least ulp / (2n) away from one, so one
+// fma rounding returns exactly the IEEE quotient (Markstein's correction).  3 fp64 ops in place
+// of the ~10-instruction v_div_scale / v_rcp / Newton / v_div_fixup sequence.  Zero, tiny,
+// huge and non-finite quotients take the IEEE divide (sign of zero, no under/overflow).
+__device__ __forceinline__ double mdiv(double x, double n, double r) {
+  const double q0 = x * r;
+  const double a = fabs(q0);
+  if (!(a >= 0x1p-960 && a <= 0x1p+1000)) return x / n;
+  const double rem = __builtin_fma(-q0, n, x);
+  return __builtin_fma(rem, r, q0);
+}
+
 struct SumSt {
   double s, ca, cr, prev;
   int n, same;                 // counts fit 32 bits (n <= D)
@@ -74,6 +89,17 @@ struct MeanSt {
       if (__builtin_signbit(v)) neg -= 1;
     }
   }
+  // result() with the division by the count through mdiv (rt[k] = RN(1 / k), k <= window)
+  __device__ double result_r(int64_t minp, const double* rt) const {
+    if (n >= minp && n > 0) {
+      double r = mdiv(s, (double)n, rt[n]);
+      if (same >= n) r = prev;
+      else if (neg == 0 && r < 0) r = 0.0;
+      else if (neg == n && r > 0) r = 0.0;
+      return r;
+    }
+    return qnan();
+  }
   __device__ double result(int64_t minp) const {
     if (n >= minp && n > 0) {
       double r = s / (double)n;
@@ -118,6 +144,43 @@ struct VarSt {
       }
     }
   }
+  // add / remove / var with every division by a count through mdiv (rt[k] = RN(1 / k))
+  __device__ void add_r(double v, const double* rt) {
+    if (v != v) return;
+    n += 1.0;
+    if (v == prev) same += 1; else same = 1;
+    prev = v;
+    double pm = mean - ca;
+    double y = v - ca;
+    double t = y - mean;
+    ca = t + mean - y;
+    mean = mean + mdiv(t, n, rt[(int)n]);
+    ssq = ssq + (v - pm) * (v - mean);
+  }
+  __device__ void remove_r(double v, const double* rt) {
+    if (v == v) {
+      n -= 1.0;
+      if (n != 0.0) {
+        double pm = mean - cr;
+        double y = v - cr;
+        double t = y - mean;
+        cr = t + mean - y;
+        mean = mean - mdiv(t, n, rt[(int)n]);
+        ssq = ssq - (v - pm) * (v - mean);
+      } else {
+        mean = 0.0;
+        ssq = 0.0;
+      }
+    }
+  }
+  __device__ double var_r(int64_t minp, int ddof, const double* rt) const {
+    if (minp < 1) minp = 1;
+    if (n >= (double)minp && n > (double)ddof) {
+      if (n == 1.0 || (double)same >= n) return 0.0;
+      return mdiv(ssq, n - (double)ddof, rt[(int)n - ddof]);
+    }
+    return qnan();
+  }
   __device__ double var(int64_t minp, int ddof) const {
     if (minp < 1) minp = 1;
     if (n >= (double)minp && n > (double)ddof) {
@@ -129,6 +192,8 @@ struct VarSt {
 };
 
 __device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v); }
+
+
 
 // ------------------------------------------------------------------------------------
 // Per-column walker state.  i counts the column's present rows.
@@ -662,10 +727,15 @@ k_ts_win(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_
 // where C = ts_corr(x, R, W) was computed for the same rows (np.sign semantics: +-0 -> +0,
 // NaN -> NaN).  The same Welford machine and operation order as k_ts_rl<STD>, so the
 // std is bit-identical to fmx_ts_op(STD) and F to the numpy restatement.
-template <int PF>
+template <int PF, bool FAST>
 __global__ void __launch_bounds__(256)
 k_ts_cvf_rl(const double* __restrict__ X, const double* __restrict__ C, double* __restrict__ Y, int64_t F,
             int64_t D, int64_t A, int64_t ld, int W) {
+  extern __shared__ double rt[];                  // FAST: [W + 1], rt[k] = RN(1 / k) (mdiv)
+  if (FAST) {
+    for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+    __syncthreads();
+  }
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (col >= F * A) return;
   const int64_t f = col / A, a = col - f * A;
@@ -689,9 +759,16 @@ k_ts_cvf_rl(const double* __restrict__ X, const double* __restrict__ C, double* 
       if (d >= D) break;
       const double vv = v[q];
       if (c.first) { c.ss.init(vv); c.ms.init(vv); c.vs.init(vv); c.first = false; }
-      if (c.i >= W) c.vs.remove(o[q]);
-      c.vs.add(vv);
-      double sd = zsqrt(c.vs.var(W, 1));
+      double sd;
+      if (FAST) {
+        if (c.i >= W) c.vs.remove_r(o[q], rt);
+        c.vs.add_r(vv, rt);
+        sd = zsqrt(c.vs.var_r(W, 1, rt));
+      } else {
+        if (c.i >= W) c.vs.remove(o[q]);
+        c.vs.add(vv);
+        sd = zsqrt(c.vs.var(W, 1));
+      }
       if (sd == 0.0) sd = qnan();
       const double cq = cv[q];
       const double sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
@@ -746,6 +823,67 @@ k_ts_corr_rl(const double* __restrict__ X, const double* __restrict__ Ycol, doub
       const double cc = (double)cnt;
       const double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (cc / (cc - 1.0));
       const double den = sqrt(vx.var(W, 1) * vy.var(W, 1));
+      o[d * ld] = num / den;
+      i += 1;
+    }
+  }
+}
+
+// ts_corr on dense panels, C5's kernel (builder-defined; pandas Rolling.corr): the same
+// machines and operation order as k_ts_corr_rl -- bit-identical -- with
+//  * every division by a window count (the three means, the two Welford mean updates per
+//    add / remove, the two variances, c / (c - 1)) through mdiv on a per-workgroup LDS table
+//    of RN(1 / k), k <= W: 10 of the 11 IEEE divides per element become 3-op corrections;
+//  * a workgroup = 4 factors x the SAME 64 assets (wave w: factor 4 g + w), so the four waves
+//    read each return row R[d], R[d - W] from the CU's L1 instead of once per factor from L2.
+constexpr int TSC_MAXW = 4096;                    // table in LDS up to this window
+template <int PF>
+__global__ void __launch_bounds__(256)
+k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ Out, int64_t F,
+               int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W, int64_t nab) {
+  extern __shared__ double rt[];                  // [W + 1]: rt[k] = RN(1 / k)
+  for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+  __syncthreads();
+  const int64_t ab = blockIdx.x % nab, fg = blockIdx.x / nab;
+  const int64_t f = fg * 4 + (threadIdx.x >> 6), a = ab * 64 + (threadIdx.x & 63);
+  if (f >= F || a >= A) return;
+  const double* x = X + f * D * ld + a;
+  const double* yc = Ycol + f * y_fstride + a;
+  double* o = Out + f * D * ld + a;
+  MeanSt mxy, mx, my;
+  VarSt vx, vy;
+  int64_t i = 0, cnt = 0;
+  bool first = true;
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double xr[PF], yr[PF], xo[PF], yo[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      xr[q] = d < D ? x[d * ld] : 0.0;
+      yr[q] = d < D ? yc[d * ld] : 0.0;
+      const bool old = d < D && d >= W;
+      xo[q] = old ? x[(d - W) * ld] : 0.0;
+      yo[q] = old ? yc[(d - W) * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      const double xv = xr[q] + 0.0 * yr[q];
+      const double yv = yr[q] + 0.0 * xr[q];
+      const double pv = xv * yv;
+      if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; }
+      if (i >= W) {
+        const double ox = xo[q] + 0.0 * yo[q], oy = yo[q] + 0.0 * xo[q];
+        mxy.remove(ox * oy); mx.remove(ox); my.remove(oy); vx.remove_r(ox, rt); vy.remove_r(oy, rt);
+        cnt -= (ox + oy == ox + oy);
+      }
+      mxy.add(pv); mx.add(xv); my.add(yv); vx.add_r(xv, rt); vy.add_r(yv, rt);
+      cnt += (xv + yv == xv + yv);
+      const double cc = (double)cnt;
+      const double ratio = cnt >= 2 ? mdiv(cc, cc - 1.0, rt[cnt - 1]) : cc / (cc - 1.0);
+      const double num = (mxy.result_r(W, rt) - mx.result_r(W, rt) * my.result_r(W, rt)) * ratio;
+      const double den = sqrt(vx.var_r(W, 1, rt) * vy.var_r(W, 1, rt));
       o[d * ld] = num / den;
       i += 1;
     }
@@ -1013,6 +1151,15 @@ extern "C" fmx_status fmx_ts_corr(const double* X, const double* Ycol, double* O
   if (!present) {   // dense: leaving values re-read at d - W
     void* rargs[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
                      (void*)&y_fstride, (void*)&W};
+    static const bool v1 = getenv("FMX_TS_CORR_V1") != nullptr;   // A/B: the round-3 kernel
+    if (W <= TSC_MAXW && !v1) {
+      int64_t nab = ceil_div(A, 64);
+      void* fargs[] = {(void*)&X, (void*)&Ycol, (void*)&Out, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
+                       (void*)&y_fstride, (void*)&W, (void*)&nab};
+      FMX_HIP(hipLaunchKernel((const void*)k_ts_corr_fast<2>, dim3((unsigned)(nab * ceil_div(F, 4))), dim3(256),
+                              fargs, sizeof(double) * (W + 1), as_stream(stream)));
+      return FMX_OK;
+    }
     // two dates of the four streams in flight: 116 VGPRs, 4 waves/SIMD (four dates: 154
     // VGPRs, 3 waves, 160 vs 156 ms at C5; eight: 180 ms; forcing 4-5 waves spills)
     const void* kc = (const void*)k_ts_corr_rl<2>;
@@ -1034,7 +1181,10 @@ extern "C" fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, 
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   int W = window;
   void* args[] = {(void*)&X, (void*)&C, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&W};
-  FMX_HIP(hipLaunchKernel((const void*)k_ts_cvf_rl<8>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args, 0,
+  static const bool v1 = getenv("FMX_TS_CORR_V1") != nullptr;   // A/B: IEEE divides
+  const bool fast = W <= TSC_MAXW && !v1;
+  FMX_HIP(hipLaunchKernel(fast ? (const void*)k_ts_cvf_rl<8, true> : (const void*)k_ts_cvf_rl<8, false>,
+                          dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args, fast ? sizeof(double) * (W + 1) : 0,
                           as_stream(stream)));
   return FMX_OK;
 }
