@@ -613,7 +613,9 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     t0 = _ev(timers)
     L = len(lags)
     if sp.world > 1:
-        per = (sp.D + sp.world - 1) // sp.world
+        # every rank pads its owned dates to the longest shard (shard_bounds' block length)
+        per = max(hi - lo for lo, hi in (shard_bounds(sp.D, sp.world, r, getattr(sp, "align", 1))
+                                          for r in range(sp.world)))
         pad = torch.zeros((L, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
         pad[..., :daily.shape[3]] = daily
         parts = sp.comm.all_gather(pad)

@@ -183,7 +183,7 @@ def test_group_moments_long_rows(dev, op, A, ragged):
     import factormodeling_amd.engine as E
     import oracle.ops as O
     rng = np.random.default_rng(A + len(op) + ragged)
-    D = 3
+    D = 4
     x = _rows(A + 1, D, A, nan=0.03)
     g = rng.integers(0, 11, size=(D, A)).astype(np.float64)
     g[rng.random(g.shape) < 0.01] = np.nan
