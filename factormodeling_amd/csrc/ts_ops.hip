@@ -32,10 +32,13 @@ namespace fmx {
 // fma rounding returns exactly the IEEE quotient (Markstein's correction).  3 fp64 ops in place
 // of the ~10-instruction v_div_scale / v_rcp / Newton / v_div_fixup sequence.  Zero, tiny,
 // huge and non-finite quotients take the IEEE divide (sign of zero, no under/overflow).
+// The range guard reads q0's biased exponent with full-rate integer ops (fp64 compares
+// issue at the quarter fp64 rate): exponents outside [64, 1958] (|q0| < 2^-959 incl. zero,
+// |q0| >= 2^936, inf, NaN) take the divide.
 __device__ __forceinline__ double mdiv(double x, double n, double r) {
   const double q0 = x * r;
-  const double a = fabs(q0);
-  if (!(a >= 0x1p-960 && a <= 0x1p+1000)) return x / n;
+  const uint32_t e = ((uint32_t)__double2hiint(q0) >> 20) & 0x7ffu;
+  if (e - 64u > 1958u - 64u) return x / n;
   const double rem = __builtin_fma(-q0, n, x);
   return __builtin_fma(rem, r, q0);
 }

@@ -17,8 +17,8 @@ static uint64_t ubits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 
 static double mdiv(double x, double n, double r) {
   const double q0 = x * r;
-  const double a = fabs(q0);
-  if (!(a >= 0x1p-960 && a <= 0x1p+1000)) return x / n;
+  const uint32_t e = (uint32_t)(ubits(q0) >> 52) & 0x7ffu;
+  if (e - 64u > 1958u - 64u) return x / n;
   const double rem = fma(-q0, n, x);
   return fma(rem, r, q0);
 }
@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
     const double nd = (double)n, r = 1.0 / nd;
     for (int i = 0; i < per; ++i) {
       double x;
-      const int kind = i % 4;
+      const int kind = i % 5;
       if (kind == 0) {                          /* random significand and exponent in +-2^60 */
         const uint64_t e = 1023 - 60 + rnd() % 121;
         x = bits((rnd() & 0x800fffffffffffffull) | (e << 52));
@@ -42,12 +42,16 @@ int main(int argc, char** argv) {
         x = bits(ubits(x) + off);
       } else if (kind == 2) {                   /* integers and halves */
         x = (double)(int64_t)(rnd() % (1ull << 52)) * (rnd() % 2 ? 0.5 : 1.0) * (rnd() % 2 ? -1.0 : 1.0);
-      } else {                                  /* O(1) data with ties to a decimal */
+      } else if (kind == 3) {                   /* O(1) data with ties to a decimal */
         x = ((double)(rnd() % 2000001) - 1000000.0) / 1000.0;
+      } else {                                  /* zeros, infinities, NaN, tiny and huge */
+        static const double sp[] = {0.0, -0.0, INFINITY, -INFINITY, NAN, 0x1p-1000, -0x1p-1060, 0x1p-960,
+                                    0x1p+1000, -0x1p+1023, 0x1.fffffffffffffp+1023, 4.9e-324};
+        x = sp[rnd() % 12] * (rnd() % 2 ? 1.0 : 3.0);
       }
       const double a = mdiv(x, nd, r), b = x / nd;
       ++tot;
-      if (ubits(a) != ubits(b)) {
+      if (ubits(a) != ubits(b) && !(a != a && b != b)) {
         if (bad < 10) fprintf(stderr, "mismatch n=%d x=%.17g: %.17g vs %.17g\n", n, x, a, b);
         ++bad;
       }

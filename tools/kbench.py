@@ -123,6 +123,8 @@ OPS = {
     "gram_exact_z": (lambda X, R, Y: E.gram_exact(Y, None), 8),
     # the C4 step's Gram straight from the panel (row stats + validity bits + tiles + popcount)
     "gram_direct": (lambda X, R, Y: E.gram_direct(X), 8),
+    # the C4 step's exact Gram (absolute 16-date blocks folded into fixed-point limbs)
+    "gram_direct_exact": (lambda X, R, Y: E.gram_direct_exact(X), 8),
     "gram_unfused": (lambda X, R, Y: E.gram(*E.zscore_exposures(X)), 8),
     "cs_stats": (lambda X, R, Y: E.cs_moment_stats("stats", X), 8),
 }
