@@ -582,6 +582,11 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if cfg.ret_ops:
         run_ret_ops(sp, cfg, timers, be, collect)
     Xs = _step_panel(sp, cfg)
+    if Xs is not sp.X:
+        # the ranks / fused IC records of the operator stage are of X, not of the feature
+        # panel the IC runs on: rank the feature panel itself below
+        side.pop("rank2", None)
+        side.pop("daily", None)
     if (cfg.rank_pass and side.get("rank2") is None and hasattr(be, "cs_rank2")
             and sp.A <= getattr(be, "rank_pass_max_a", 0)):
         # no operator ranked X this step: one ranks-only pass feeds the IC (inside the pass

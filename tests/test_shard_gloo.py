@@ -160,3 +160,45 @@ def test_local_comm_shards_match_gloo_semantics(world):
         assert np.array_equal(C, col["C"].numpy())
         for k, v in ops.items():
             np.testing.assert_allclose(v, col[k].numpy()[:, lo:hi], rtol=1e-12, atol=1e-12, equal_nan=True, err_msg=k)
+
+
+def test_feature_panel_step_never_reuses_the_ranks_of_x():
+    """a step that ranks X in its operator set AND builds the C5 feature panel
+    must not feed X's ranks (or X's fused IC records) to the IC of the feature panel."""
+    import torch
+    from factormodeling_amd import pipeline as PL
+
+    calls = []
+
+    class Be:
+        ranked_ic_max_a = 1 << 30
+
+        def cs_rank_winsor(self, X, outs, rank2=None):
+            outs[0].zero_()
+            outs[1].zero_()
+            if rank2 is not None:
+                rank2.zero_()
+
+        def op(self, kind, op, w, X, out):
+            out.copy_(X)
+
+        def ts_corr_into(self, X, R, w, out):
+            out.fill_(0.5)
+
+        def corr_vol_feature(self, X, C, w, out):
+            out.copy_(X * 2.0)
+
+        def ic_daily(self, X, R, lags, rank2=None):
+            calls.append((X.data_ptr(), rank2))
+            return torch.zeros((len(lags), 4, X.shape[0], X.shape[1]), dtype=X.dtype)
+
+        def ic_window(self, daily, d0, d1):
+            return torch.zeros((len(d0), daily.shape[1], 8), dtype=daily.dtype)
+
+    cfg = PL.StepConfig(ops=[("cs_rank", None, None), ("winsor", None, None)], ret_ops=[("corr_vol", 5)],
+                        select=False, gram=False, ic_lags=(1,))
+    sp = PL.ShardedPanel(30, 8, 3, 0, 1, torch.device("cpu"), seed=1, halo=cfg.halo)
+    PL.run_step(sp, cfg, be=Be())
+    assert len(calls) == 1
+    ptr, rank2 = calls[0]
+    assert ptr == sp.feature.data_ptr() and rank2 is None
