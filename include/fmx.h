@@ -104,7 +104,8 @@ fmx_status fmx_device_info(char* buf, int64_t buflen);
 /* ---- time series (operations.py:6-51) -------------------------------------------- */
 /* Replaces ts_sum/ts_mean/ts_std/ts_zscore/ts_rank/ts_decay/ts_diff/ts_delay/ts_backfill
  * (operations.py:6-51).  Y may not alias X.  Rolling sums/means/variances reproduce
- * pandas' Kahan/Welford kernels bit-for-bit. */
+ * pandas' Kahan/Welford kernels bit-for-bit.  Any window (no LDS ring: DESIGN §12), dense
+ * or ragged; window < 0 for diff / delay is a lead. */
 fmx_status fmx_ts_op(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                      int32_t window, const uint8_t* present, void* stream);
 
