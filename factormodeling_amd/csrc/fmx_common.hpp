@@ -51,6 +51,24 @@ __device__ __forceinline__ double okey_inv(uint64_t k) {
 }
 constexpr uint64_t KEY_SENTINEL = 0xffffffffffffffffull;  // sorts after +inf
 
+// RN(x / n) for an integer n >= 1 from r = RN(1 / n) (a table entry): q0 = RN(x r) is within
+// 1.5 ulp of x / n; the remainder x - q0 n is exact under an fma; q0 + r (x - q0 n) lies
+// within 1.5 * 2^-53 ulp of x / n, which is never a rounding midpoint (x / n = odd * 2^(e-1)
+// would need x to carry more than 53 bits) and sits at least ulp / (2n) away from one, so one
+// fma rounding returns exactly the IEEE quotient (Markstein's correction).  3 fp64 ops in place
+// of the ~10-instruction v_div_scale / v_rcp / Newton / v_div_fixup sequence.  Zero, tiny,
+// huge and non-finite quotients take the IEEE divide (sign of zero, no under/overflow).
+// The range guard reads q0's biased exponent with full-rate integer ops (fp64 compares
+// issue at the quarter fp64 rate): exponents outside [64, 1958] (|q0| < 2^-959 incl. zero,
+// |q0| >= 2^936, inf, NaN) take the divide.
+__device__ __forceinline__ double mdiv(double x, double n, double r) {
+  const double q0 = x * r;
+  const uint32_t e = ((uint32_t)__double2hiint(q0) >> 20) & 0x7ffu;
+  if (e - 64u > 1958u - 64u) return x / n;
+  const double rem = __builtin_fma(-q0, n, x);
+  return __builtin_fma(rem, r, q0);
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -60,10 +60,25 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
 
 // Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
 // raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
+// Rows of 8193..10240 assets (C5) take the persistent k_cs_rank2_pf (one row per CU, the
+// next row's loads in flight, no spills); FMX_RANK2_PF=0 keeps k_cs_rank_fa for A/B.
+static bool rank2_pf_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("FMX_RANK2_PF");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
   const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
+  if (nt_fa == 1024 && E == 10 && rank_impl() == RANK_IMPL_FINE && rank2_pf_enabled()) {
+    int64_t nrows = F * D;
+    void* args[] = {(void*)&X, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&RK};
+    return launch_persistent((const void*)k_cs_rank2_pf<1024, 10>, 1024, nrows, lds_fr, args, st);
+  }
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense)(nt_fa, E);
   if (!k || !lds_fits(k, lds_fr)) { set_error("fmx_cs_rank2: A <= 16384"); return FMX_ERR_UNSUPPORTED; }
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }

@@ -15,8 +15,11 @@
 namespace fmx {
 
 // min waves per SIMD of the aliased-LDS cs_rank kernel: three rows per CU
+#ifndef FR_FA_WAVES1024
+#define FR_FA_WAVES1024 8
+#endif
 #ifndef FR_FA_WAVES
-#define FR_FA_WAVES(NT) ((NT) == 1024 ? 8 : ((NT) == 640 ? 8 : 6))
+#define FR_FA_WAVES(NT) ((NT) == 1024 ? FR_FA_WAVES1024 : ((NT) == 640 ? 8 : 6))
 #endif
 // ... but no more than the LDS lets in: a row stages up to EMAX*NT 8-byte keys (at least
 // the 32 KB counter array), so long rows (EMAX*NT > 6144) hold one or two rows per CU
@@ -29,12 +32,27 @@ constexpr int fr_fa_min_waves(int nt, int emax) {
   const int w = rows * nt / 256;
   return w < 1 ? 1 : (w > FR_FA_WAVES(nt) ? FR_FA_WAVES(nt) : w);
 }
+// Row slot k of thread t holds position t + k*NT.  br_emax rounds ceil(A / NT) up to the
+// next instantiated EMAX (7 -> 8, 9 -> 10, 11 -> 12, 13..15 -> 16, ...), so any slot, not
+// just the last, may lie past the row's end: every slot is tested, and the unconditional
+// loads are clamped into the row.
+template <int NT>
+__device__ __forceinline__ bool fr_in(int t, int k, int A) { return t + k * NT < A; }
+template <int NT>
+__device__ __forceinline__ int fr_ix(int t, int k, int A) {
+  const int i = t + k * NT;
+  return i < A ? i : (A > 0 ? A - 1 : 0);
+}
 // Scheduling fence between unrolled per-element steps: bounds how many elements' live
 // ranges overlap (register pressure at 8 waves/SIMD) -- other waves hide the latency.
 #ifndef FR_NO_SCHED_FENCE
 #define FR_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define FR_SCHED_FENCE() (void)0
+#endif
+// in-bucket scan of k_cs_rank_fa: one loop per element slot (1) or one loop over all (0)
+#ifndef FR_SCAN_PERK
+#define FR_SCAN_PERK 1
 #endif
 constexpr int FR_K_CS = 247;   // fine buckets per interval (cs_rank: 16-bit counters, 32 KB)
 constexpr int FR_CS_WORDS = 8192;
@@ -131,16 +149,15 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
     }
   }
   // lag 0's returns in flight over the table build
-  const bool last_ok = last_in;
+  (void)last_in;
   auto pair_of = [&](int k, int m) {           // non-NaN exposure (r2 > 0), non-NaN return
-    return (k < EMAX - 1 || last_ok) && fr_r2<EMAX>(r2, k) != 0u && !((em >> (2 * k + m)) & 1);
+    return fr_in<NT>(t, k, (int)A) && fr_r2<EMAX>(r2, k) != 0u && !((em >> (2 * k + m)) & 1);
   };
   // unconditional loads (a branch per load serialises them): the last slot clamped into
   // the row, inactive lags read date s's row; non-pairs are skipped when summing
-  const int ilast = (EMAX - 1) * NT + t < (int)A ? (EMAX - 1) * NT + t : (int)A - 1;
   auto load_r = [&](double* rv, const double* rr) {
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) rv[k] = rr[k < EMAX - 1 ? t + k * NT : ilast];
+    for (int k = 0; k < EMAX; ++k) rv[k] = rr[fr_ix<NT>(t, k, (int)A)];
   };
   double rv[EMAX];
   load_r(rv, ic.Rt + (rw.act[0] ? rw.s + rw.lag[0] : rw.s) * ld);
@@ -152,7 +169,7 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
     // a long NaN-return list: k_ic_ranked_list takes the row from its doubled ranks
 #pragma unroll
     for (int k = 0; k < EMAX; ++k)
-      if (k < EMAX - 1 || last_in) ic.RK[row * ld + t + k * NT] = (fmx_rank2_t)fr_r2<EMAX>(r2, k);
+      if (fr_in<NT>(t, k, (int)A)) ic.RK[row * ld + t + k * NT] = (fmx_rank2_t)fr_r2<EMAX>(r2, k);
     if (t == 0) {
       const int q = atomicAdd(&ic.ovf[0], 1);
       ic.ovf[1 + q] = (int32_t)blockIdx.x;
@@ -365,18 +382,17 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   // every load of the row issued before the first is consumed: a load under a branch (the
   // key conversion below is one per element) waits out the previous one's HBM latency.
   // The last slot is clamped into the row (its value is unused when out of range).
-  const int ilast = last_in ? t + (EMAX - 1) * NT : (An > 0 ? An - 1 : 0);
   double xv[EMAX];
   uint32_t pv = 0;
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? fr_opaque(t) + k * NT : ilast];
+  for (int k = 0; k < EMAX; ++k) xv[k] = x[fr_ix<NT>(fr_opaque(t), k, (int)A)];
   if (PRES) {
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) pv |= (prow[k < EMAX - 1 ? t + k * NT : ilast] != 0 ? 1u : 0u) << k;
+    for (int k = 0; k < EMAX; ++k) pv |= (prow[fr_ix<NT>(t, k, (int)A)] != 0 ? 1u : 0u) << k;
   }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const bool in = k < EMAX - 1 || last_in;
+    const bool in = fr_in<NT>(t, k, (int)A);
     const double v = xv[k];
     const bool p = in && (PRES ? ((pv >> k) & 1u) != 0 : true);
     const bool ok = p && v == v;
@@ -415,17 +431,17 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if (Y) {                                  // Y == NULL: doubled ranks only (fmx_cs_rank2)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) y[fr_opaque(t) + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
+        if (fr_in<NT>(t, k, (int)A)) y[fr_opaque(t) + k * NT] = (((pm >> k) & 1) && half) ? 0.5 : qnan();
     }
     if (RK) {                                 // nv == 0 or a single-row date (rank 1)
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) RK[row * ld + fr_opaque(t) + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
+        if (fr_in<NT>(t, k, (int)A)) RK[row * ld + fr_opaque(t) + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
     }
     if (WQ) {                                 // nv < 5: winsor is the identity
 #pragma unroll
       for (int k = 0; k < EMAX; ++k)
-        if (k < EMAX - 1 || last_in) Y2[row * ld + fr_opaque(t) + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
+        if (fr_in<NT>(t, k, (int)A)) Y2[row * ld + fr_opaque(t) + k * NT] = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
     }
     if constexpr (IC) {                       // < 3 pairs: empty records (n = 0, or 1 on a one-asset row)
       if (t == 0) {
@@ -484,6 +500,25 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   }
   __syncthreads();
   BR_PH();
+#if FR_SCAN_PERK
+  // one exec-masked loop per element slot: a wave runs sum_k max_lanes(n_k) short
+  // iterations instead of max_lanes max_k(n_k) iterations over all EMAX slots
+  (void)maxlen;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) {
+    const int n = sl[k] >> 16;
+    if (n) {
+      const uint64_t* bk = bkey + (sl[k] & 0xffff);
+      const uint64_t own = key[k];
+      int acc = 0;
+      for (int j = 0; j < n; ++j) {
+        const uint64_t w = bk[j];
+        acc += (w < own ? 1 : 0) + (w == own ? 0x10000 : 0);
+      }
+      le[k] = acc;
+    }
+  }
+#else
   for (int j = 0; j < maxlen; ++j) {
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
@@ -493,7 +528,9 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       }
     }
   }
+#endif
   const double den = (double)(nrow - 1);
+  const double rden = 1.0 / den;              // (r - 1) / den through mdiv: bit-identical
   // winsor order statistics (numpy linear) of the nv valid keys
   __shared__ uint64_t tval[4];
   int kk[4] = {0, 0, 0, 0};
@@ -519,7 +556,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     if constexpr (IC) if (k % 2 == 0) r2[k / 2] = 0u;
-    if (!(k < EMAX - 1 || last_in)) continue;
+    if (!fr_in<NT>(t, k, (int)A)) continue;
     const int lt = le[k] & 0xffff, eq = le[k] >> 16;
     const int less = (sl[k] & 0xffff) + lt;
     if constexpr (IC) r2[k / 2] |= (key[k] != KEY_SENTINEL ? (uint32_t)(2 * less + eq + 1) : 0u) << (16 * (k % 2));
@@ -529,7 +566,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     else r = (double)less + (double)(eq + 1) / 2.0;
     // write-once outputs: nontemporal stores
     const int ia = fr_opaque(t) + k * NT;       // recomputed here, not kept from the loads
-    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : (r - 1.0) / den, y + ia);
+    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : mdiv(r - 1.0, den, rden), y + ia);
     if (RK) __builtin_nontemporal_store((fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1)),
                                         RK + row * ld + ia);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
@@ -546,9 +583,9 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       const uint32_t* nb = ic.nanb + (rw.s + rw.lag[m]) * ic.nw;
 #pragma unroll
       for (int k = 0; k < EMAX; ++k) {
-        const int i = (k < EMAX - 1 || last_in) ? t + k * NT : 0;   // unconditional loads
+        const int i = fr_in<NT>(t, k, (int)A) ? t + k * NT : 0;   // unconditional loads
         const uint32_t bit = (nb[i >> 5] >> (i & 31)) & 1u;
-        if ((k < EMAX - 1 || last_in) && key[k] != KEY_SENTINEL) em |= bit << (2 * k + m);
+        if (fr_in<NT>(t, k, (int)A) && key[k] != KEY_SENTINEL) em |= bit << (2 * k + m);
       }
     }
   }
@@ -570,7 +607,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     double* y2 = Y2 + row * ld;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      if (!(k < EMAX - 1 || last_in)) continue;
+      if (!fr_in<NT>(t, k, (int)A)) continue;
       const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
       double o = v;
       if (nv >= 5) o = (v < lo) ? lo : ((v > hi) ? hi : v);
@@ -583,7 +620,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     double* xk = reinterpret_cast<double*>(lds);
 #pragma unroll
     for (int k = 0; k < EMAX; ++k)
-      if (k < EMAX - 1 || last_in) xk[t + k * NT] = key[k] != KEY_SENTINEL ? okey_inv(key[k]) : 0.0;
+      if (fr_in<NT>(t, k, (int)A)) xk[t + k * NT] = key[k] != KEY_SENTINEL ? okey_inv(key[k]) : 0.0;
     // exposure anchor: a sample key of the row (block-uniform, the sorted samples in tab)
     const uint64_t sk = tab.spl[31] != KEY_SENTINEL ? tab.spl[31] : tab.spl[0];
     const double xs = sk != KEY_SENTINEL ? okey_inv(sk) : 0.0;
@@ -592,6 +629,149 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
                          reinterpret_cast<uint32_t*>(lds) + fr_ic_xk_words(A), ic_ne BR_PH_ARGS);
   }
   BR_PH();
+}
+
+// Bucket ids of a thread's keys, group by group (fr_bucket_grp), each group's LDS counter
+// increments issued right away: sl[k] = slot | bucket << PK_BSHIFT.  The scheduling fence
+// keeps the compiler from interleaving every group's searches and final selects (all EMAX
+// sample words in flight at once).
+template <int K, int EMAX, int G>
+__device__ __forceinline__ void fr_bucket_cnt(const FrTab& T, const uint64_t* key, int* sl, int dummy,
+                                              uint32_t* cnt) {
+  constexpr int g = EMAX < G ? EMAX : G;
+  int b[g];
+  fr_bucket_grp<K, g>(T, key, b, dummy);
+#pragma unroll
+  for (int k = 0; k < g; ++k) sl[k] = (int)fr_cnt_add(cnt, b[k]) | (b[k] << PK_BSHIFT);
+  FR_SCHED_FENCE();
+  if constexpr (EMAX > G) fr_bucket_cnt<K, EMAX - G, G>(T, key + G, sl + G, dummy, cnt);
+}
+
+// ------------------------------------------------------------------------------------
+// Doubled average ranks only, persistent (fmx_cs_rank2 on rows of 8193..16384 assets: the
+// rank pass in front of a daily IC over a panel no operator ranks, e.g. C5's feature panel).
+// One 1024-thread workgroup per CU walks rows b, b + G, ...; the next row's loads are issued
+// as soon as the current row's keys are formed and land during its bucket phases (its HBM
+// latency was the exposed third of a row's time).  At one row per CU the kernel has 128
+// VGPRs: keys, the prefetched row and the per-element state fit without spills (two rows
+// per CU at 64 VGPRs spilled the keys).  Bucket pipeline and per-element results as
+// k_cs_rank_fa (dense, method average, RK only):
+//   rank2 = 2 * #less + #equal + 1 (0 for NaN); single-asset rows -> 2.
+template <int NT, int EMAX>
+__global__ void __launch_bounds__(NT, 4)
+k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld, fmx_rank2_t* __restrict__ RK) {
+  constexpr int K = FR_K_CS, NW = NT / 64;
+  constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;
+  static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
+  __shared__ FrTab tab;
+  __shared__ uint4 wred[NW];
+  __shared__ int iscr[NW];
+  extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters)
+  uint32_t* cnt = (uint32_t*)lds;
+  uint64_t* bkey = lds;
+  const int t = threadIdx.x, wid = t >> 6;
+  const int An = (int)A;
+  double xv[EMAX];
+  int64_t row = blockIdx.x;
+  if (row >= nrows) return;
+#pragma unroll
+  for (int k = 0; k < EMAX; ++k) xv[k] = X[row * ld + (fr_ix<NT>(fr_opaque(t), k, (int)A))];
+  for (; row < nrows; row += gridDim.x) {
+    uint64_t key[EMAX];
+    uint32_t hmin = 0xffffffffu, hmax = 0u;
+    int wv = 0;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const double v = xv[k];
+      const bool ok = fr_in<NT>(t, k, (int)A) && v == v;
+      key[k] = ok ? okey(v) : KEY_SENTINEL;
+      const uint32_t h = (uint32_t)(key[k] >> 32);
+      hmin = ok ? min(hmin, h) : hmin;
+      hmax = ok ? max(hmax, h) : hmax;
+      wv += __popcll(__ballot(ok));
+    }
+    {                                         // the next row's loads (clamped to the last row)
+      const int64_t nxt = row + gridDim.x < nrows ? row + gridDim.x : row;
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k) xv[k] = X[nxt * ld + (fr_ix<NT>(fr_opaque(t), k, (int)A))];
+    }
+    fr_park_sample<NT, EMAX>(tab, key);
+    __syncthreads();                          // the previous row's scan reads of bkey are done
+#pragma unroll
+    for (int j = 0; j < WORDS / (4 * NT); ++j)
+      reinterpret_cast<uint4*>(cnt)[t * (WORDS / (4 * NT)) + j] = make_uint4(0u, 0u, 0u, 0u);
+    {
+      const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
+      if ((t & 63) == 0) wred[wid] = make_uint4(0u, (uint32_t)wv, a, c);
+    }
+    __syncthreads();
+    int nv = 0;
+    uint32_t h0 = 0xffffffffu, h1 = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint4 r = wred[w];
+      nv += (int)r.y;
+      h0 = min(h0, r.z);
+      h1 = max(h1, r.w);
+    }
+    fmx_rank2_t* rk = RK + row * ld;
+    if (nv == 0 || An == 1) {                 // no valid key / a single-asset row (rank 1)
+#pragma unroll
+      for (int k = 0; k < EMAX; ++k)
+        if (fr_in<NT>(t, k, (int)A)) rk[fr_opaque(t) + k * NT] = (fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : 2u);
+      continue;                               // block-uniform
+    }
+    if (wid == 0) {
+      double vmin, vmax;
+      fr_key_bounds(h0, h1, &vmin, &vmax);
+      fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
+    }
+    __syncthreads();
+    int sl[EMAX];
+    fr_bucket_cnt<K, EMAX, 4>(tab, key, sl, DUMMY, cnt);
+    __syncthreads();
+    fr_scan16<NT, WORDS>(cnt, iscr);
+    int le[EMAX];                             // scatter slot, then c = 2 #less + #equal in the bucket
+    uint32_t nan_m = 0;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int b = sl[k] >> PK_BSHIFT;
+      const int slot = sl[k] & PK_SLOT;
+      const int s0 = (int)fr_cnt_get(cnt, b);
+      const int n = (int)fr_cnt_get(cnt, b + 1) - s0;
+      const bool eqb = (b % (K + 1)) == K;    // equal-to-sample bucket: all members tie
+      const bool scan = !eqb && n > 1 && b != DUMMY;
+      nan_m |= (uint32_t)(b == DUMMY) << k;
+      le[k] = scan ? slot : (eqb ? n : 1);
+      sl[k] = s0 | (scan ? n << 16 : 0);
+    }
+    __syncthreads();                          // counters dead: the keys reuse their LDS
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (sl[k] >> 16) bkey[(sl[k] & 0xffff) + le[k]] = key[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int n = sl[k] >> 16;
+      if (n) {
+        const uint64_t* bk = bkey + (sl[k] & 0xffff);
+        const uint64_t own = bk[le[k]];       // own key from its slot: keys dead after the scatter
+        int c = 0;
+#pragma unroll 2
+        for (int j = 0; j < n; ++j) {
+          const uint64_t w = bk[j];
+          c += (w < own ? 2 : 0) + (w == own ? 1 : 0);
+        }
+        le[k] = c;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      if (!fr_in<NT>(t, k, (int)A)) continue;
+      const uint32_t r2 = ((nan_m >> k) & 1u) ? 0u : (uint32_t)(2 * (sl[k] & 0xffff) + le[k] + 1);
+      __builtin_nontemporal_store((fmx_rank2_t)r2, rk + fr_opaque(t) + k * NT);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -628,24 +808,21 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
   const double* x = X + row * ld;
   double* y = Y + row * ld;
   const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
-  const int An = (int)A;
-  const bool last_in = t + (EMAX - 1) * NT < An;
   uint64_t key[EMAX];
   uint32_t pm = 0, hmin = 0xffffffffu, hmax = 0u;
   int wv = 0;
   // all loads in flight before the first is consumed (as k_cs_rank_fa)
-  const int ilast = last_in ? t + (EMAX - 1) * NT : (An > 0 ? An - 1 : 0);
   double xv[EMAX];
   uint32_t pv = 0;
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) xv[k] = x[k < EMAX - 1 ? t + k * NT : ilast];
+  for (int k = 0; k < EMAX; ++k) xv[k] = x[fr_ix<NT>(t, k, (int)A)];
   if (PRES) {
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) pv |= (prow[k < EMAX - 1 ? t + k * NT : ilast] != 0 ? 1u : 0u) << k;
+    for (int k = 0; k < EMAX; ++k) pv |= (prow[fr_ix<NT>(t, k, (int)A)] != 0 ? 1u : 0u) << k;
   }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const bool in = k < EMAX - 1 || last_in;
+    const bool in = fr_in<NT>(t, k, (int)A);
     const double v = xv[k];
     const bool p = in && (PRES ? ((pv >> k) & 1u) != 0 : true);
     const bool ok = p && v == v;
@@ -774,7 +951,7 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
   }
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    if (!(k < EMAX - 1 || last_in)) continue;
+    if (!fr_in<NT>(t, k, (int)A)) continue;
     const double v = key[k] == KEY_SENTINEL ? qnan() : okey_inv(key[k]);
     double o;
     if (OP == 0) {
@@ -872,10 +1049,9 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
   int cw0 = 0, cw1 = 0;                       // wave-uniform pair counts per lag
   // the row's exposures are all in flight before the first is consumed
-  const bool last_in = t + (EMAX - 1) * NT < A;
   double xv[EMAX];
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) xv[k] = (k < EMAX - 1 || last_in) ? xf[t + k * NT] : qnan();
+  for (int k = 0; k < EMAX; ++k) xv[k] = fr_in<NT>(t, k, (int)A) ? xf[t + k * NT] : qnan();
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
     const int i = t + k * NT;
@@ -1116,10 +1292,9 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
 #pragma unroll
   for (int q = 0; q < 8; ++q) mx[q] = -INFINITY;
   int cw0 = 0, cw1 = 0;
-  const bool last_in = t + (EMAX - 1) * NT < A;
   double xv[EMAX];
 #pragma unroll
-  for (int k = 0; k < EMAX; ++k) xv[k] = (k < EMAX - 1 || last_in) ? xf[t + k * NT] : qnan();
+  for (int k = 0; k < EMAX; ++k) xv[k] = fr_in<NT>(t, k, (int)A) ? xf[t + k * NT] : qnan();
   __syncthreads();                            // ecnt zeroed
   uint32_t pm = 0, em = 0;                    // per element: pair / E mask of each lag
 #pragma unroll
@@ -1180,7 +1355,7 @@ __device__ __forceinline__ void ic_ranked_row(int64_t row, const double* __restr
     // doubled ranks (loads in flight over the E sort)
     uint32_t rk[EMAX];
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) rk[k] = (k < EMAX - 1 || last_in) ? rkf[t + k * NT] : 0u;
+    for (int k = 0; k < EMAX; ++k) rk[k] = fr_in<NT>(t, k, (int)A) ? rkf[t + k * NT] : 0u;
     const int ne[2] = {__builtin_amdgcn_readfirstlane(ecnt[0]), __builtin_amdgcn_readfirstlane(ecnt[1])};
     const int nw = wid == 0 ? ne[0] : ne[1];
     if (wid < 2 && nw > 0 && nw < ES) {

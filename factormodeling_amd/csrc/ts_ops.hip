@@ -25,24 +25,6 @@
 
 namespace fmx {
 
-// RN(x / n) for an integer n >= 1 from r = RN(1 / n) (a table entry): q0 = RN(x r) is within
-// 1.5 ulp of x / n; the remainder x - q0 n is exact under an fma; q0 + r (x - q0 n) lies
-// within 1.5 * 2^-53 ulp of x / n, which is never a rounding midpoint (x / n = odd * 2^(e-1)
-// would need x to carry more than 53 bits) and sits at least ulp / (2n) away from one, so one
-// fma rounding returns exactly the IEEE quotient (Markstein's correction).  3 fp64 ops in place
-// of the ~10-instruction v_div_scale / v_rcp / Newton / v_div_fixup sequence.  Zero, tiny,
-// huge and non-finite quotients take the IEEE divide (sign of zero, no under/overflow).
-// The range guard reads q0's biased exponent with full-rate integer ops (fp64 compares
-// issue at the quarter fp64 rate): exponents outside [64, 1958] (|q0| < 2^-959 incl. zero,
-// |q0| >= 2^936, inf, NaN) take the divide.
-__device__ __forceinline__ double mdiv(double x, double n, double r) {
-  const double q0 = x * r;
-  const uint32_t e = ((uint32_t)__double2hiint(q0) >> 20) & 0x7ffu;
-  if (e - 64u > 1958u - 64u) return x / n;
-  const double rem = __builtin_fma(-q0, n, x);
-  return __builtin_fma(rem, r, q0);
-}
-
 struct SumSt {
   double s, ca, cr, prev;
   int n, same;                 // counts fit 32 bits (n <= D)
@@ -189,6 +171,75 @@ struct VarSt {
     if (n >= (double)minp && n > (double)ddof) {
       if (n == 1.0 || (double)same >= n) return 0.0;
       return ssq / (n - (double)ddof);
+    }
+    return qnan();
+  }
+};
+
+// One side (x or y) of ts_corr: a MeanSt and a VarSt fed the same values, sharing what the
+// two machines track identically -- the NaN test, the count, the run of equal values and
+// its value -- so each add / remove does that bookkeeping once.  Every arithmetic step is
+// the two machines' own, in their order (bit-identical results).
+struct MVSt {
+  double s, cam, crm;          // MeanSt: Kahan sum and its add / remove compensations
+  double mean, ssq, cav, crv;  // VarSt: Welford mean, sum of squares, compensations
+  double prev;
+  int n, neg, same;
+  __device__ void init(double first) {
+    s = cam = crm = mean = ssq = cav = crv = 0.0;
+    n = neg = same = 0;
+    prev = first;
+  }
+  __device__ void add_r(double v, const double* rt) {
+    if (v == v) {
+      n += 1;
+      const double y = v - cam, t = s + y;
+      cam = t - s - y; s = t;
+      if (__builtin_signbit(v)) neg += 1;
+      if (v == prev) same += 1; else same = 1;
+      prev = v;
+      const double pm = mean - cav;
+      const double y2 = v - cav;
+      const double t2 = y2 - mean;
+      cav = t2 + mean - y2;
+      mean = mean + mdiv(t2, (double)n, rt[n]);
+      ssq = ssq + (v - pm) * (v - mean);
+    }
+  }
+  __device__ void remove_r(double v, const double* rt) {
+    if (v == v) {
+      n -= 1;
+      const double y = -v - crm, t = s + y;
+      crm = t - s - y; s = t;
+      if (__builtin_signbit(v)) neg -= 1;
+      if (n != 0) {
+        const double pm = mean - crv;
+        const double y2 = v - crv;
+        const double t2 = y2 - mean;
+        crv = t2 + mean - y2;
+        mean = mean - mdiv(t2, (double)n, rt[n]);
+        ssq = ssq - (v - pm) * (v - mean);
+      } else {
+        mean = 0.0;
+        ssq = 0.0;
+      }
+    }
+  }
+  __device__ double mean_r(int64_t minp, const double* rt) const {   // MeanSt::result_r
+    if (n >= minp && n > 0) {
+      double r = mdiv(s, (double)n, rt[n]);
+      if (same >= n) r = prev;
+      else if (neg == 0 && r < 0) r = 0.0;
+      else if (neg == n && r > 0) r = 0.0;
+      return r;
+    }
+    return qnan();
+  }
+  __device__ double var_r(int64_t minp, int ddof, const double* rt) const {   // VarSt::var_r
+    if (minp < 1) minp = 1;
+    if (n >= minp && n > ddof) {
+      if (n == 1 || same >= n) return 0.0;
+      return mdiv(ssq, (double)(n - ddof), rt[n - ddof]);
     }
     return qnan();
   }
@@ -853,8 +904,8 @@ k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, do
   const double* x = X + f * D * ld + a;
   const double* yc = Ycol + f * y_fstride + a;
   double* o = Out + f * D * ld + a;
-  MeanSt mxy, mx, my;
-  VarSt vx, vy;
+  MeanSt mxy;
+  MVSt sx, sy;
   int64_t i = 0, cnt = 0;
   bool first = true;
   for (int64_t d0 = 0; d0 < D; d0 += PF) {
@@ -875,18 +926,18 @@ k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, do
       const double xv = xr[q] + 0.0 * yr[q];
       const double yv = yr[q] + 0.0 * xr[q];
       const double pv = xv * yv;
-      if (first) { mxy.init(pv); mx.init(xv); my.init(yv); vx.init(xv); vy.init(yv); first = false; }
+      if (first) { mxy.init(pv); sx.init(xv); sy.init(yv); first = false; }
       if (i >= W) {
         const double ox = xo[q] + 0.0 * yo[q], oy = yo[q] + 0.0 * xo[q];
-        mxy.remove(ox * oy); mx.remove(ox); my.remove(oy); vx.remove_r(ox, rt); vy.remove_r(oy, rt);
+        mxy.remove(ox * oy); sx.remove_r(ox, rt); sy.remove_r(oy, rt);
         cnt -= (ox + oy == ox + oy);
       }
-      mxy.add(pv); mx.add(xv); my.add(yv); vx.add_r(xv, rt); vy.add_r(yv, rt);
+      mxy.add(pv); sx.add_r(xv, rt); sy.add_r(yv, rt);
       cnt += (xv + yv == xv + yv);
       const double cc = (double)cnt;
       const double ratio = cnt >= 2 ? mdiv(cc, cc - 1.0, rt[cnt - 1]) : cc / (cc - 1.0);
-      const double num = (mxy.result_r(W, rt) - mx.result_r(W, rt) * my.result_r(W, rt)) * ratio;
-      const double den = sqrt(vx.var_r(W, 1, rt) * vy.var_r(W, 1, rt));
+      const double num = (mxy.result_r(W, rt) - sx.mean_r(W, rt) * sy.mean_r(W, rt)) * ratio;
+      const double den = sqrt(sx.var_r(W, 1, rt) * sy.var_r(W, 1, rt));
       o[d * ld] = num / den;
       i += 1;
     }

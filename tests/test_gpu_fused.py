@@ -287,6 +287,35 @@ def test_cs_rank2_matches_rank_winsor_ranks(dev, A):
     assert np.array_equal(got.cpu().numpy(), ref.cpu().numpy())
 
 
+@pytest.mark.parametrize("A", [8193, 10000, 10240])
+def test_cs_rank2_persistent_rows_vs_rankdata(dev, A):
+    """The persistent ranks-only kernel (k_cs_rank2_pf: one row per CU, the next row's loads
+    in flight) over more rows than the grid holds, with heavy ties, NaN, empty and
+    single-value rows: doubled average ranks = 2 * scipy rankdata(average), 0 for NaN."""
+    import torch
+    from scipy.stats import rankdata
+    import factormodeling_amd.engine as E
+    rng = np.random.default_rng(A)
+    F, D = 2, 300                                # 600 rows > 256 CUs
+    X = rng.standard_normal((F, D, A))
+    X[:, ::3] = np.round(X[:, ::3], 1)           # tie-heavy rows
+    X[:, 1::7] = np.round(X[:, 1::7] * 3)        # few distinct values
+    X[rng.random(X.shape) < 0.03] = np.nan
+    X[0, 5] = np.nan                             # empty row
+    X[1, 9, 1:] = np.nan                         # single valid value
+    X[1, 11] = 2.5                               # one value
+    Xt = torch.as_tensor(X, device=dev)
+    got = E.cs_rank2(Xt).cpu().numpy().astype(np.int64)
+    for f in range(F):
+        for d in range(D):
+            x = X[f, d]
+            ok = ~np.isnan(x)
+            exp = np.zeros(A, dtype=np.int64)
+            if ok.any():
+                exp[ok] = np.rint(2 * rankdata(x[ok], method="average")).astype(np.int64)
+            assert np.array_equal(got[f, d], exp), (f, d)
+
+
 def test_ts_set_division_edge_values(dev):
     """The fused rolling set is bit-identical to the single-op kernels on zero / signed-zero
     / huge / subnormal-range / infinite values, exact ties and a large offset."""

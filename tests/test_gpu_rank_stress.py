@@ -13,6 +13,9 @@ from golden_io import assert_close
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 2, 3, 7, 64, 511, 512, 513, 1500, 5000, 10000, 16384]
+# rows whose ceil(A / NT) is not an instantiated EMAX (rounded up 7 -> 8, 9 -> 10, 11 -> 12,
+# 13..15 -> 16 at NT = 512 / 1024): slots before the last one run past the row's end
+ROUNDED = [3500, 4600, 5600, 7000, 8193, 9000, 11000, 13000]
 NPAT = 12
 
 
@@ -58,7 +61,7 @@ def eng():
     return E, torch
 
 
-@pytest.mark.parametrize("A", SIZES)
+@pytest.mark.parametrize("A", SIZES + ROUNDED)
 def test_cs_rank_stress(eng, A):
     import oracle.ops as O
     E, torch = eng
@@ -110,7 +113,7 @@ def test_cs_rank_sorted_equals_bitonic(eng):
         assert np.array_equal(Y.cpu().numpy(), ref.cpu().numpy(), equal_nan=True), method
 
 
-@pytest.mark.parametrize("A", SIZES)
+@pytest.mark.parametrize("A", SIZES + ROUNDED)
 def test_cs_quantile_stress(eng, A):
     import oracle.ops as O
     E, torch = eng
@@ -122,7 +125,7 @@ def test_cs_quantile_stress(eng, A):
     assert_close(got.ravel(), O.cs_filter_center(x).ravel(), exact=True, what=f"filter_center A={A}")
 
 
-@pytest.mark.parametrize("A", [3, 7, 513, 1500, 5000])
+@pytest.mark.parametrize("A", [3, 7, 513, 1500, 5000, 3500, 9000])
 def test_ic_daily_stress(eng, A):
     import oracle.metrics as OM
     E, torch = eng
@@ -146,3 +149,31 @@ def test_ic_daily_stress(eng, A):
             assert out[li, 0, 0, t] == n
             assert_close(out[li, 1:, 0, t], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12,
                          what=f"A={A} L={L} t={t}")
+
+
+@pytest.mark.parametrize("A", [5000, 10000] + ROUNDED)
+def test_cs_rank_winsor_rank2_stress(eng, A):
+    """The fused rank + winsor pass (and its doubled ranks) and the ranks-only pass on the
+    adversarial rows: rank / winsor bit-exact vs the oracle, doubled ranks = 2 * the
+    average rank (0 for NaN) from both passes."""
+    import oracle.ops as O
+    E, torch = eng
+    x = adversarial_rows(A, A + 5)
+    keep = np.ones(len(x), bool)
+    keep[6] = False                        # +-inf: fine for ranks, kept out of winsor's lerp
+    x = x[keep]
+    Xd = torch.as_tensor(x[None], device="cuda")
+    rk = torch.empty(Xd.shape, dtype=E.RANK2_DTYPE, device="cuda")
+    yr, yw = E.cs_rank_winsor(Xd, 0.01, 0.99, rank2=rk)
+    assert_close(yr.cpu().numpy()[0].ravel(), O.cs_rank(x).ravel(), exact=True, what=f"rank A={A}")
+    assert_close(yw.cpu().numpy()[0].ravel(), O.cs_winsor(x).ravel(), exact=True, what=f"winsor A={A}")
+    from scipy.stats import rankdata
+    exp = np.zeros(x.shape, np.int64)
+    for d in range(len(x)):
+        ok = ~np.isnan(x[d])
+        if ok.any():
+            exp[d, ok] = np.rint(2 * rankdata(x[d, ok], method="average")).astype(np.int64)
+    got = rk.cpu().numpy()[0].astype(np.uint16).astype(np.int64)
+    assert np.array_equal(got, exp), f"rank2 (fused) A={A}"
+    got2 = E.cs_rank2(Xd).cpu().numpy()[0].astype(np.uint16).astype(np.int64)
+    assert np.array_equal(got2, exp), f"rank2 (ranks-only) A={A}"
