@@ -61,6 +61,8 @@ def bytes_per_unit(stage, F, ranked=False):
         return 10.0
     if stage.startswith("ret:cvf"):     # C5 feature: X (+ the leaving value) and ts_corr in, F out
         return 24.0
+    if stage.startswith("ret:corr_vol"):  # C5 fused ts_corr -> feature: X once + F out (R amortised)
+        return 16.0
     if kind == "ret":                # ts_corr / ts_std vs returns: X once + out (R amortised)
         return 16.0
     if kind == "ic_daily":              # X once (+ its u16 ranks when ranked) + two R rows
@@ -70,8 +72,8 @@ def bytes_per_unit(stage, F, ranked=False):
 
 # stage -> kernel-name prefix in the rocprofv3 PMC summaries (profiles/traffic_c*.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
-                "ts_set": "fmx::k_ts_set<", "rank2": ("fmx::k_cs_rank_fa<1024, 10, false, false", "fmx::k_cs_rank_fa<"),
-                "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
+                "ts_set": "fmx::k_ts_set<", "rank2": ("fmx::k_cs_rank2_pf<", "fmx::k_cs_rank_fa<1024, 10, false, false", "fmx::k_cs_rank_fa<"),
+                "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:corr_vol": "fmx::k_ts_corr_feat<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
                 "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
                 "rank_ic": "fmx::k_cs_rank_fa<",

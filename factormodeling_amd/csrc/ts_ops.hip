@@ -944,6 +944,75 @@ k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, do
   }
 }
 
+// C5's feature in the ts_corr pass (fmx_ts_corr_feature): k_ts_corr_fast's machines and
+// layout (bit-identical corr) plus the feature's own ts_std(x, W) machine on the raw x
+// (k_ts_cvf_rl's VarSt, same order), so the feature
+//     sign(corr) * (x / ts_std(x, W))      (ts_std 0 -> NaN; np.sign of a NaN corr is NaN)
+// is written while the corr is in registers: the corr panel is not written and read back,
+// and x / x[d - W] are read once for both.  C (optional) also receives the corr.
+template <int PF>
+__global__ void __launch_bounds__(256)
+k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ C,
+               double* __restrict__ Out, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W,
+               int64_t nab) {
+  extern __shared__ double rt[];                  // [W + 1]: rt[k] = RN(1 / k)
+  for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+  __syncthreads();
+  const int64_t ab = blockIdx.x % nab, fg = blockIdx.x / nab;
+  const int64_t f = fg * 4 + (threadIdx.x >> 6), a = ab * 64 + (threadIdx.x & 63);
+  if (f >= F || a >= A) return;
+  const double* x = X + f * D * ld + a;
+  const double* yc = Ycol + f * y_fstride + a;
+  double* o = Out + f * D * ld + a;
+  double* cp = C ? C + f * D * ld + a : nullptr;
+  MeanSt mxy;
+  MVSt sx, sy;
+  VarSt vs;                                       // ts_std(x, W) of the raw x (the feature's)
+  int64_t i = 0, cnt = 0;
+  bool first = true;
+  for (int64_t d0 = 0; d0 < D; d0 += PF) {
+    double xr[PF], yr[PF], xo[PF], yo[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      xr[q] = d < D ? x[d * ld] : 0.0;
+      yr[q] = d < D ? yc[d * ld] : 0.0;
+      const bool old = d < D && d >= W;
+      xo[q] = old ? x[(d - W) * ld] : 0.0;
+      yo[q] = old ? yc[(d - W) * ld] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t d = d0 + q;
+      if (d >= D) break;
+      const double xv = xr[q] + 0.0 * yr[q];
+      const double yv = yr[q] + 0.0 * xr[q];
+      const double pv = xv * yv;
+      if (first) { mxy.init(pv); sx.init(xv); sy.init(yv); vs.init(xr[q]); first = false; }
+      if (i >= W) {
+        const double ox = xo[q] + 0.0 * yo[q], oy = yo[q] + 0.0 * xo[q];
+        mxy.remove(ox * oy); sx.remove_r(ox, rt); sy.remove_r(oy, rt);
+        cnt -= (ox + oy == ox + oy);
+        vs.remove_r(xo[q], rt);
+      }
+      mxy.add(pv); sx.add_r(xv, rt); sy.add_r(yv, rt);
+      cnt += (xv + yv == xv + yv);
+      vs.add_r(xr[q], rt);
+      const double cc = (double)cnt;
+      const double ratio = cnt >= 2 ? mdiv(cc, cc - 1.0, rt[cnt - 1]) : cc / (cc - 1.0);
+      const double num = (mxy.result_r(W, rt) - sx.mean_r(W, rt) * sy.mean_r(W, rt)) * ratio;
+      const double den = sqrt(sx.var_r(W, 1, rt) * sy.var_r(W, 1, rt));
+      const double cq = num / den;
+      if (cp) __builtin_nontemporal_store(cq, cp + d * ld);
+      double sd = zsqrt(vs.var_r(W, 1, rt));
+      if (sd == 0.0) sd = qnan();
+      const double sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
+      __builtin_nontemporal_store(sg * (xr[q] / sd), o + d * ld);
+      i += 1;
+    }
+  }
+}
+
 // W == 0: diff -> x - x, delay -> x, decay -> x (no window).
 __global__ void k_ts_window0(const double* __restrict__ X, double* __restrict__ Y, int64_t n_total,
                              int op, const uint8_t* __restrict__ present, int64_t DA, int64_t ld) {
@@ -1239,6 +1308,29 @@ extern "C" fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, 
   const bool fast = W <= TSC_MAXW && !v1;
   FMX_HIP(hipLaunchKernel(fast ? (const void*)k_ts_cvf_rl<8, true> : (const void*)k_ts_cvf_rl<8, false>,
                           dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args, fast ? sizeof(double) * (W + 1) : 0,
+                          as_stream(stream)));
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_ts_corr_feature(const double* X, const double* Ycol, double* C, double* Y, int64_t F,
+                                          int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int32_t window,
+                                          void* stream) {
+  FMX_ARG(X && Ycol && Y, "null panel");
+  FMX_ARG(Y != X && Y != Ycol && (!C || (C != X && C != Ycol && C != Y)), "outputs must not alias the inputs");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A, "bad dims");
+  FMX_ARG(window >= 1 && window <= TSC_MAXW, "window must be in [1, 4096]");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  int W = window;
+  int64_t nab = ceil_div(A, 64);
+  void* args[] = {(void*)&X, (void*)&Ycol, (void*)&C, (void*)&Y, (void*)&F, (void*)&D, (void*)&A, (void*)&ld,
+                  (void*)&y_fstride, (void*)&W, (void*)&nab};
+  // one date in flight: 106 VGPRs, 4 waves/SIMD (two: 130 VGPRs, 3 waves); FMX_CORR_FEAT_PF=2 for A/B
+  static const bool pf2 = [] {
+    const char* e = getenv("FMX_CORR_FEAT_PF");
+    return e && e[0] == '2';
+  }();
+  FMX_HIP(hipLaunchKernel(pf2 ? (const void*)k_ts_corr_feat<2> : (const void*)k_ts_corr_feat<1>,
+                          dim3((unsigned)(nab * ceil_div(F, 4))), dim3(256), args, sizeof(double) * (W + 1),
                           as_stream(stream)));
   return FMX_OK;
 }

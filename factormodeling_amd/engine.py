@@ -93,6 +93,30 @@ def ts_corr(X, Ycol, window: int, present=None, out=None):
     return out
 
 
+def corr_feature(X, Ycol, window: int, out=None, corr_out=None):
+    """C5's feature sign(ts_corr(X, Ycol, window)) * (X / ts_std(X, window)) in one pass
+    (fmx_ts_corr_feature): bit-identical to ts_corr + corr_vol_feature, without the corr
+    panel's round trip.  ``corr_out`` (optional) also receives the corr.  Dense panels."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    if Ycol.dim() == 2:
+        if tuple(Ycol.shape) != (D, A):
+            raise _lib.FmxError("Ycol must be [D][A] or [F][D][A]")
+        ystride = 0
+    else:
+        if tuple(Ycol.shape) != (F, D, A):
+            raise _lib.FmxError("Ycol must be [D][A] or [F][D][A]")
+        ystride = D * A
+    Ycol = Ycol.contiguous()
+    out = _out(X, out)
+    if corr_out is not None:
+        corr_out = _out(X, corr_out)
+    call("fmx_ts_corr_feature", ptr(X), ptr(Ycol), ptr(corr_out), ptr(out), F, D, A, A, ystride, int(window),
+         stream_ptr())
+    return out
+
+
 def corr_vol_feature(X, C, window: int, out=None):
     """C5's feature sign(C) * (X / ts_std(X, window)) (fmx_ts_corr_vol_feature); C is
     ts_corr(X, R, window) of the same rows (same shape as X)."""

@@ -370,6 +370,10 @@ class EngineBackend:
     def corr_vol_feature(X, C, w, out):
         E.corr_vol_feature(X, C, w, out=out)
 
+    @staticmethod
+    def corr_feature_into(X, R, w, out, corr_out=None):
+        E.corr_feature(X, R, w, out=out, corr_out=corr_out)
+
     wcomp = staticmethod(E.wcomp)
     ic_daily = staticmethod(E.ic_daily)
     ic_window = staticmethod(E.ic_window)
@@ -490,10 +494,10 @@ def _rec(timers, name, t0):
 def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
     """Operators against the returns over factor chunks of ``cfg.factor_chunk`` (a
     full-size output per operator would not fit next to a 100 GB panel): ("corr", w) /
-    ("std", w) write reused chunk buffers; ("corr_vol", w) -- C5 -- writes ts_corr(x, R, w)
-    of the chunk into a chunk buffer and then the chunk of the feature panel sp.feature =
-    sign(ts_corr) * x / ts_std(x, w) (fmx_ts_corr_vol_feature), which the rest of the step
-    runs on."""
+    ("std", w) write reused chunk buffers; ("corr_vol", w) -- C5 -- writes the chunk of the
+    feature panel sp.feature = sign(ts_corr(x, R, w)) * x / ts_std(x, w) in one pass
+    (fmx_ts_corr_feature; a backend without it: ts_corr into a chunk buffer, then
+    fmx_ts_corr_vol_feature), which the rest of the step runs on."""
     F = sp.X.shape[0]
     fc = cfg.factor_chunk or F
     n = min(fc, F)
@@ -510,6 +514,14 @@ def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
         for (op, w), buf in zip(cfg.ret_ops, bufs):
             out = buf[: f1 - f0]
             t0 = _ev(timers)
+            if op == "corr_vol" and hasattr(be, "corr_feature_into"):
+                # one pass: the corr stays in registers (written only when collected)
+                want = collect is not None and collect.get("_factors") is None
+                be.corr_feature_into(Xc, sp.R, w, sp.feature[f0:f1], out if want else None)
+                _rec(timers, f"ret:corr_vol:{w}", t0)
+                if want:
+                    collect.setdefault(f"ret:corr:{w}", []).append(out[:, sp.halo:].clone())
+                continue
             if op in ("corr", "corr_vol"):
                 be.ts_corr_into(Xc, sp.R, w, out)
             else:

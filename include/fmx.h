@@ -146,6 +146,13 @@ fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F
  * Dense panels. */
 fmx_status fmx_ts_corr_vol_feature(const double* X, const double* C, double* Y, int64_t F, int64_t D, int64_t A,
                                    int64_t ld, int32_t window, void* stream);
+/* The same feature straight from the returns in ONE pass (C5's chain: ts_corr of x with
+ * Ycol feeding sign(corr) * x / ts_std(x, window), pipeline.ipynb's corr-vol signal): the
+ * corr panel is neither written nor re-read.  Y is bit-identical to fmx_ts_corr (dense) +
+ * fmx_ts_corr_vol_feature; C, when not NULL, also receives the corr.  Dense panels,
+ * 1 <= window <= 4096, Ycol as in fmx_ts_corr (y_fstride 0: one [D][ld] return panel). */
+fmx_status fmx_ts_corr_feature(const double* X, const double* Ycol, double* C, double* Y, int64_t F, int64_t D,
+                               int64_t A, int64_t ld, int64_t y_fstride, int32_t window, void* stream);
 /* cs_zscore (Yz) and market_neutralize (Yn) of the same rows from ONE set of moments
  * (operations.py:77-78, :171-182); optional stats[F][D][2] = (mean, std ddof=0).  Outputs
  * bit-identical to fmx_cs_moment of each op; distinct from X and each other. */

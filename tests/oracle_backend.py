@@ -43,6 +43,11 @@ class OracleBackend:
                 out[f] = torch.from_numpy(np.sign(c[f]) * (x[f] / np.where(s == 0, np.nan, s)))
         return out
 
+    def corr_feature_into(self, X, R, w, out, corr_out=None):
+        """The fused pass: ts_corr then the feature (the oracle has no fusion to mirror)."""
+        c = self.ts_corr_into(X, R, w, torch.empty_like(X) if corr_out is None else corr_out)
+        return self.corr_vol_feature(X, c, w, out)
+
     def weighted_composite(self, X, names, pdate, w, method):
         """weighted_composite_factor of each processed day's selection (owned dates only)."""
         import oracle.composite as OC

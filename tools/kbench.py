@@ -116,6 +116,7 @@ OPS = {
                                                                                             device=X.device))), 24),
     "ts_corr60": (lambda X, R, Y: E.ts_corr(X, R, 60, out=Y), 16),
     "cvf60": (lambda X, R, Y: E.corr_vol_feature(X, Y, 60, out=_set_outs(X)["mean"]), 24),
+    "corr_feat60": (lambda X, R, Y: E.corr_feature(X, R, 60, out=Y), 16),
     "rank2": (lambda X, R, Y: E.cs_rank2(X, _RK.setdefault("rk2", torch.empty(X.shape, dtype=E.RANK2_DTYPE,
                                                                               device=X.device))), 10),
     "gram": (lambda X, R, Y: E.corr_matrix(X), 8),
