@@ -571,6 +571,80 @@ k_ts_rl(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_t
   }
 }
 
+// ts_mean / ts_std / ts_zscore of one window from ONE MeanSt + VarSt pair (fmx_ts_set's
+// moments for any window, dense or ragged): the machines, their order and every output's
+// arithmetic are ts_moment's MEAN / STD / ZSCORE paths, so each output is bit-identical to
+// its single-op pass.  Outputs may be NULL.
+__device__ __forceinline__ void ts_mom3_step(ColState& c, double v, double old, int W, double* ym, double* ys,
+                                             double* yz) {
+  if (c.first) { c.ms.init(v); c.vs.init(v); c.first = false; }
+  if (c.i >= W) { c.ms.remove(old); c.vs.remove(old); }
+  c.ms.add(v); c.vs.add(v);
+  const double m = c.ms.result(W);
+  const double sd = zsqrt(c.vs.var(W, 1));
+  if (ym) __builtin_nontemporal_store(m, ym);
+  if (ys) __builtin_nontemporal_store(sd, ys);
+  if (yz) __builtin_nontemporal_store((v - m) / (sd == 0.0 ? qnan() : sd), yz);
+  c.i += 1;
+}
+
+// Dense: the leaving value re-read at d - W (k_ts_rl), PF dates of both streams in flight;
+// ragged (present != NULL): the trailing row pointer of k_ts_ptr, absent rows NaN.
+template <int PF>
+__global__ void __launch_bounds__(256)
+k_ts_mom3(const double* __restrict__ X, double* __restrict__ Ym, double* __restrict__ Ys, double* __restrict__ Yz,
+          int64_t F, int64_t D, int64_t A, int64_t ld, int W, const uint8_t* __restrict__ present) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= F * A) return;
+  const int64_t f = col / A, a = col - f * A;
+  const int64_t base = f * D * ld + a;
+  const double* x = X + base;
+  double* ym = Ym ? Ym + base : nullptr;
+  double* ys = Ys ? Ys + base : nullptr;
+  double* yz = Yz ? Yz + base : nullptr;
+  ColState c;
+  c.init();
+  if (!present) {
+    for (int64_t d0 = 0; d0 < D; d0 += PF) {
+      double v[PF], o[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int64_t d = d0 + q;
+        v[q] = d < D ? x[d * ld] : 0.0;
+        o[q] = (d < D && d >= W) ? x[(d - W) * ld] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int64_t d = d0 + q;
+        if (d >= D) break;
+        ts_mom3_step(c, v[q], o[q], W, ym ? ym + d * ld : nullptr, ys ? ys + d * ld : nullptr,
+                     yz ? yz + d * ld : nullptr);
+      }
+    }
+    return;
+  }
+  const uint8_t* pres = present + a;
+  int64_t tail = -1;
+  double oldv = 0.0;
+  for (int64_t d = 0; d < D; ++d) {
+    const double v = x[d * ld];
+    if (pres[d * ld] == 0) {
+      if (ym) ym[d * ld] = qnan();
+      if (ys) ys[d * ld] = qnan();
+      if (yz) yz[d * ld] = qnan();
+      continue;
+    }
+    if (tail < 0) { tail = d; oldv = v; }
+    double old = 0.0;
+    if (c.i >= W) {
+      old = oldv;
+      do { ++tail; } while (pres[tail * ld] == 0);
+      oldv = x[tail * ld];
+    }
+    ts_mom3_step(c, v, old, W, ym ? ym + d * ld : nullptr, ys ? ys + d * ld : nullptr, yz ? yz + d * ld : nullptr);
+  }
+}
+
 // Ragged panels (a presence byte per (date, asset); absent rows are not part of the
 // symbol's row sequence, operations.py's groupby('symbol') walk): the same column walk,
 // with the value leaving the window found by a TRAILING ROW POINTER -- the date of the
@@ -1252,9 +1326,20 @@ extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, d
                             0, as_stream(stream)));
     return FMX_OK;
   }
-  // other windows / ragged panels: one single-op pass per requested output
+  // other windows / ragged panels: the three moments from one pair of machines (one pass),
+  // then ts_rank and ts_decay on their own best kernels (any window); FMX_TS_SET_SPLIT=1:
+  // one single-op pass per output (A/B)
   const int32_t ops[5] = {FMX_TS_MEAN, FMX_TS_STD, FMX_TS_ZSCORE, FMX_TS_RANK, FMX_TS_DECAY};
-  for (int k = 0; k < 5; ++k) {
+  int k0 = 0;
+  if (getenv("FMX_TS_SET_SPLIT") == nullptr && (Ymean || Ystd || Yzscore)) {
+    int W = window;
+    void* args[] = {(void*)&X, (void*)&Ymean, (void*)&Ystd, (void*)&Yzscore, (void*)&F, (void*)&D, (void*)&A,
+                    (void*)&ld, (void*)&W, (void*)&present};
+    FMX_HIP(hipLaunchKernel((const void*)k_ts_mom3<4>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args, 0,
+                            as_stream(stream)));
+    k0 = 3;
+  }
+  for (int k = k0; k < 5; ++k) {
     if (!outs[k]) continue;
     fmx_status e = fmx_ts_op(ops[k], X, outs[k], F, D, A, ld, k == 3 ? rank_window : window, present, stream);
     if (e) return e;

@@ -25,7 +25,8 @@ def _panel(seed, F, D, A):
     return X
 
 
-@pytest.mark.parametrize("D,A,W,WR", [(97, 700, 20, 10), (23, 129, 20, 10), (61, 300, 5, 5), (40, 65, 20, 20)])
+@pytest.mark.parametrize("D,A,W,WR", [(97, 700, 20, 10), (23, 129, 20, 10), (61, 300, 5, 5), (40, 65, 20, 20),
+                                      (200, 131, 60, 20), (400, 70, 150, 80)])
 def test_ts_set_matches_single_ops(dev, D, A, W, WR):
     import torch
     import factormodeling_amd.engine as E
@@ -47,11 +48,15 @@ def test_ts_set_subset_and_ragged(dev):
     assert np.array_equal(outs["zscore"].cpu().numpy(), E.ts("zscore", X, 20).cpu().numpy(), equal_nan=True)
     assert np.array_equal(outs["decay"].cpu().numpy(), E.ts("decay", X, 20).cpu().numpy(), equal_nan=True)
     pres = torch.as_tensor((np.random.default_rng(1).random((50, 200)) > 0.2).astype(np.uint8), device=dev)
-    outs = {k: torch.empty_like(X) for k in E.TS_SET}
-    E.ts_set(X, outs, 20, 10, pres)
-    for k in E.TS_SET:
-        ref = E.ts(k, X, 10 if k == "rank" else 20, pres).cpu().numpy()
-        assert np.array_equal(outs[k].cpu().numpy(), ref, equal_nan=True), k
+    for W, WR in ((20, 10), (7, 3), (45, 30)):   # ragged: the one-pass moments + rank + decay
+        outs = {k: torch.empty_like(X) for k in E.TS_SET}
+        E.ts_set(X, outs, W, WR, pres)
+        for k in E.TS_SET:
+            ref = E.ts(k, X, WR if k == "rank" else W, pres).cpu().numpy()
+            assert np.array_equal(outs[k].cpu().numpy(), ref, equal_nan=True), (k, W, WR)
+    outs = {"std": torch.empty_like(X)}             # a moments subset on the general path
+    E.ts_set(X, outs, 33, 10)
+    assert np.array_equal(outs["std"].cpu().numpy(), E.ts("std", X, 33).cpu().numpy(), equal_nan=True)
 
 
 def _cs_panel(seed, F, D, A):

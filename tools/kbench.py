@@ -107,6 +107,7 @@ OPS = {
     "winsor": (lambda X, R, Y: E.cs_quantile_op("winsor", X, 0.01, 0.99, out=Y), 16),
     "ic": (lambda X, R, Y: E.ic_daily(X, R, (1, 2)), 8),
     "ts_set": (lambda X, R, Y: E.ts_set(X, _set_outs(X), 20, 10), 48),
+    "ts_set60_20": (lambda X, R, Y: E.ts_set(X, _set_outs(X), 60, 20), 48),
     "cs_zn": (lambda X, R, Y: E.cs_zscore_neutralize(X, Y, _set_outs(X)["mean"]), 24),
     "cs_rw": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"]), 24),
     "cs_rw_rk": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"], rank2=_rank2(X)), 26),
