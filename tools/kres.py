@@ -12,7 +12,7 @@ import re
 import subprocess
 import sys
 
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
+FLAGS = [*__import__("os").environ.get("KRES_DEFS", "").split(), "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
          "-Wno-unused-function", "-munsafe-fp-atomics"]
 
 
