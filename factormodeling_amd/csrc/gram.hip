@@ -524,7 +524,6 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
       while (j >= NB - bi) { j -= NB - bi; ++bi; }
       blk[u] = bi | ((bi + j) << 8);
     }
-    blk[u] = __builtin_amdgcn_readfirstlane(blk[u]);   // wave-uniform: SGPRs, scalar branches
   }
   dbl4 gacc[BPW];
 #pragma unroll
