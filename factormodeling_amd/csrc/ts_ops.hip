@@ -348,13 +348,15 @@ __device__ __forceinline__ double ts_step_reg(ColState& c, double v, double* rin
         less += (ring[k] < v);
         eq += (ring[k] == v);
       }
-      out = ((double)less + (double)(eq + 1) / 2.0) / (double)W;
+      constexpr double RW = 1.0 / (double)W;             // constant divisor: mdiv (bit-identical)
+      out = mdiv((double)less + (double)(eq + 1) / 2.0, (double)W, RW);
     } else {
       // oldest element sits in slot q+1 (mod W); weights 1..W oldest->newest
       double acc = 0.0;
 #pragma unroll
       for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);   // as BLAS ddot
-      out = acc / ((double)W * (double)(W + 1) / 2.0);
+      constexpr double DEN = (double)W * (double)(W + 1) / 2.0, RDEN = 1.0 / DEN;
+      out = mdiv(acc, DEN, RDEN);
     }
   } else if (OP == FMX_TS_DIFF) {
     out = (c.i >= W) ? v - old : qnan();
@@ -471,7 +473,8 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
         less += (w < v);
         eq += (w == v);
       }
-      o = ((double)less + (double)(eq + 1) / 2.0) / (double)WR;
+      constexpr double RWR = 1.0 / (double)WR;           // constant divisor: mdiv (bit-identical)
+      o = mdiv((double)less + (double)(eq + 1) / 2.0, (double)WR, RWR);
     }
     __builtin_nontemporal_store(o, Yr + off);
   }
@@ -481,7 +484,8 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
       double acc = 0.0;
 #pragma unroll
       for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);
-      o = acc / ((double)W * (double)(W + 1) / 2.0);
+      constexpr double DEN = (double)W * (double)(W + 1) / 2.0, RDEN = 1.0 / DEN;
+      o = mdiv(acc, DEN, RDEN);
     }
     __builtin_nontemporal_store(o, Yd + off);
   }
@@ -836,14 +840,15 @@ k_ts_win(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_
   if (!ok) return;
   double* y = Y + f * D * ld + a;
   const double den = (double)W * (double)(W + 1) / 2.0;
+  const double rden = 1.0 / den, rw = 1.0 / Wd;         // once per thread: mdiv below
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int d = d0 + t;
     if (d >= d1) break;
     double o = qnan();
     if (((pm >> t) & 1u) && qW[t] >= -1.0) {            // a full window of W present rows
-      if (OP == FMX_TS_DECAY) o = acc[t] / den;         // NaN in the window propagates
-      else if (s2[t] < TSW_NANBIT) o = ((double)(s2[t] + 1) / 2.0) / Wd;
+      if (OP == FMX_TS_DECAY) o = mdiv(acc[t], den, rden);   // NaN in the window propagates
+      else if (s2[t] < TSW_NANBIT) o = mdiv((double)(s2[t] + 1) / 2.0, Wd, rw);
     }
     y[(int64_t)d * ld] = o;
   }
