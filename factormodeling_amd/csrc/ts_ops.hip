@@ -432,9 +432,19 @@ k_ts_reg(const double* __restrict__ X, double* __restrict__ Y, int64_t F, int64_
 #ifndef TS_SET_WAVES
 #define TS_SET_WAVES 4
 #endif
+// TS_SET_MV (default): the set's mean and std machines as one MVSt pair (shared NaN test,
+// count and equal-run bookkeeping) with every count division through mdiv on an LDS table
+// of RN(1 / k); 0: separate MeanSt / VarSt with IEEE divides (A/B).  Bit-identical.
+#ifndef TS_SET_MV
+#define TS_SET_MV 1
+#endif
 struct SetSt {
+#if TS_SET_MV
+  MVSt mv;
+#else
   MeanSt ms;
   VarSt vs;
+#endif
   int64_t i;
   int nan_w, nan_r;
   bool first;
@@ -444,17 +454,26 @@ template <int W, int WR>
 __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, int q, int64_t off,
                                             double* __restrict__ Ym, double* __restrict__ Ys,
                                             double* __restrict__ Yz, double* __restrict__ Yr,
-                                            double* __restrict__ Yd) {
-  if (c.first) { c.ms.init(v); c.vs.init(v); c.first = false; }
+                                            double* __restrict__ Yd, const double* rt) {
   const bool full = c.i >= W;
   const double old = full ? ring[q] : qnan();
   // element leaving the rank window (still in the ring when WR < W)
   const double oldr = (WR == W) ? old : ((c.i >= WR) ? ring[(q + W - WR) % W] : qnan());
   ring[q] = v;
+#if TS_SET_MV
+  if (c.first) { c.mv.init(v); c.first = false; }
+  if (full) c.mv.remove_r(old, rt);
+  c.mv.add_r(v, rt);
+  const double m = c.mv.mean_r(W, rt);
+  const double sd = zsqrt(c.mv.var_r(W, 1, rt));
+#else
+  (void)rt;
+  if (c.first) { c.ms.init(v); c.vs.init(v); c.first = false; }
   if (full) { c.ms.remove(old); c.vs.remove(old); }
   c.ms.add(v); c.vs.add(v);
   const double m = c.ms.result(W);
   const double sd = zsqrt(c.vs.var(W, 1));
+#endif
   // outputs are written once and not re-read by this kernel: nontemporal (streaming)
   // stores, +11 % on this 1-read / 5-write column walk (tools/colwalk.hip)
   if (Ym) __builtin_nontemporal_store(m, Ym + off);
@@ -498,6 +517,9 @@ __global__ void __launch_bounds__(256, TS_SET_WAVES)
 k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restrict__ Ys, double* __restrict__ Yz,
          double* __restrict__ Yr, double* __restrict__ Yd, int64_t F, int64_t D, int64_t A, int64_t ld) {
   static_assert(W % PF == 0 && WR >= 1 && WR <= W, "windows");
+  __shared__ double rt[W + 1];                // RN(1 / k), k <= W (mdiv)
+  for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+  __syncthreads();
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (col >= F * A) return;
   const int64_t f = col / A, a = col - f * A;
@@ -520,7 +542,7 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
       const double v = pf[q % PF];
       pf[q % PF] = __builtin_nontemporal_load(xp);
       xp += ld;
-      ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
+      ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd, rt);
       off += ld;
       asm volatile("" : "+v"(off));   // no per-step address precomputation (spills)
     }
@@ -533,7 +555,7 @@ k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restri
         const double v = pf[q % PF];
         if (d + PF < D) pf[q % PF] = __builtin_nontemporal_load(xp);
         xp += ld;
-        ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd);
+        ts_set_step<W, WR>(c, v, ring, q, off, Ym, Ys, Yz, Yr, Yd, rt);
         off += ld;
       asm volatile("" : "+v"(off));   // no per-step address precomputation (spills)
       }
