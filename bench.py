@@ -53,6 +53,8 @@ def bytes_per_unit(stage, F, ranked=False):
         return 24.0
     if kind == "cs_rank_winsor":        # X once + two outputs + the doubled ranks (u16)
         return 26.0 if ranked else 24.0
+    if kind == "cs_rank_winsor_zn":     # X once + four outputs + the doubled ranks (u16)
+        return 42.0 if ranked else 40.0
     if kind == "cs_rank_winsor_ic":     # X once + two outputs + two R rows per (f, date); no ranks
         return 24.0 + 16.0 / F
     if kind == "rank_ic":               # ranks-only pass with the IC fused: X once + two R rows
@@ -76,6 +78,7 @@ STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic
                 "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:corr_vol": "fmx::k_ts_corr_feat<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
                 "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
+                "cs_rank_winsor_zn": "fmx::k_cs_rank_fa<512, 10, false, true, false, true>",
                 "rank_ic": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",

@@ -836,6 +836,28 @@ extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double*
   return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
 }
 
+extern "C" fmx_status fmx_cs_rank_winsor_zn(const double* X, double* Yrank, double* Ywinsor, double* Yz, double* Yn,
+                                            int64_t F, int64_t D, int64_t A, int64_t ld, double qlo, double qhi,
+                                            fmx_rank2_t* rank2, void* stream) {
+  FMX_ARG(X && Yrank && Ywinsor && Yz && Yn, "null panel");
+  const double* outs[4] = {Yrank, Ywinsor, Yz, Yn};
+  for (int i = 0; i < 4; ++i) {
+    FMX_ARG(outs[i] != X, "outputs must be distinct from X");
+    for (int j = i + 1; j < 4; ++j) FMX_ARG(outs[i] != outs[j], "outputs must be distinct from each other");
+  }
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 65535, "bad dims");
+  if (F == 0 || D == 0 || A == 0) return FMX_OK;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  e = br_cs_rank_winsor_zn(X, Yrank, Ywinsor, Yz, Yn, F, D, A, ld, qlo, qhi, rank2, pw, pw_len((int)A),
+                           as_stream(stream));
+  if (e != FMX_ERR_UNSUPPORTED) return e;
+  // rows the fused kernel does not take: rank + winsor, then the moments
+  if ((e = fmx_cs_rank_winsor(X, Yrank, Ywinsor, F, D, A, ld, qlo, qhi, nullptr, rank2, stream))) return e;
+  return fmx_cs_zscore_neutralize(X, Yz, Yn, F, D, A, ld, nullptr, nullptr, stream);
+}
+
 extern "C" fmx_status fmx_cs_rank2(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
                                    void* stream) {
   FMX_ARG(X && rank2, "null panel");

@@ -28,8 +28,9 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   double qlo = 0.0, qhi = 0.0;
   fmx_rank2_t* RK = nullptr;
   FrIc ic{};
+  FrZn zn{};
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
@@ -51,8 +52,33 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   if (F * D == 0) return FMX_OK;
   int method = FMX_RANK_AVERAGE;
   FrIc ic{};
+  FrZn zn{};
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
+  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  return FMX_OK;
+}
+
+// cs_rank + cs_winsor (+ doubled ranks) + cs_zscore + market_neutralize of dense rows in one
+// pass (k_cs_rank_fa<ZN>); FMX_ERR_UNSUPPORTED when the row does not fit the fine kernel.
+template <int NT, int E> constexpr auto kcrwz_dense = k_cs_rank_fa<NT, E, false, true, false, true>;
+fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double* Yz, double* Yn, int64_t F, int64_t D,
+                                int64_t A, int64_t ld, double qlo, double qhi, fmx_rank2_t* RK, PwTable pw, int slen,
+                                hipStream_t st) {
+  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
+  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
+  const int E = br_emax(A, nt_fa);
+  const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcrwz_dense)(nt_fa, E);
+  if (rank_impl() == RANK_IMPL_BR || !k || !lds_fits(k, lds_fr)) return FMX_ERR_UNSUPPORTED;
+  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (F * D == 0) return FMX_OK;
+  int method = FMX_RANK_AVERAGE;
+  const uint8_t* present = nullptr;
+  FrIc ic{};
+  FrZn zn{Yz, Yn, pw, slen};
+  void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;
@@ -89,8 +115,9 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   const uint8_t* present = nullptr;
   double qlo = 0.0, qhi = 0.0;
   FrIc ic{};
+  FrZn zn{};
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   return FMX_OK;

@@ -72,6 +72,15 @@ struct FrIc {
   int32_t* ovf;              // [1 + F*D]: rows whose NaN-return list exceeds FR_IC_EC
   fmx_rank2_t* RK;           // the doubled ranks of those rows (k_ic_ranked_list input)
 };
+// cs_zscore + market_neutralize fused into the rank + winsor pass (k_cs_rank_fa<..., ZN>):
+// the row's numpy moments from the same load (operations.py:77-78, :171-182).
+struct FrZn {
+  double* Yz;                // cs_zscore output
+  double* Yn;                // market_neutralize output
+  PwTable pw;                // numpy pairwise schedules (the row length's)
+  int slen;                  // its length in int32 words
+};
+constexpr int FR_ZN_NODES = 2 * (16384 / 64) + 8;
 constexpr int FR_IC_EC = 256;  // E entries per lag held in LDS; longer lists: ovf
 #ifndef FR_IC_CH
 #define FR_IC_CH 2             // return loads in flight per thread in the IC pass
@@ -347,11 +356,17 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
 //
 // IC (dense rows, method average): the daily IC records of the row's two lags from its
 // ranks (fr_ic_tail) -- no doubled ranks written, no second pass over X.
-template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false>
+//
+// ZN (dense rows, with WQ): cs_zscore and market_neutralize of the same rows too -- the row is
+// staged once in LDS (the region the counters take next) for numpy's pairwise nansum and
+// sum of squared deviations (block_pw_sum_w0, bit-identical to k_cs_moment_rg), and the two
+// outputs are written from it before the ranking starts: the row is read from HBM once for
+// four operators (fmx_cs_rank_winsor_zn).
+template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false, bool ZN = false>
 __global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
-             fmx_rank2_t* __restrict__ RK, FrIc ic) {
+             fmx_rank2_t* __restrict__ RK, FrIc ic, FrZn zn) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
@@ -364,6 +379,10 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
   static_assert(!(IC && PRES), "the fused IC ranks dense rows");
+  static_assert(!ZN || (WQ && !PRES && !IC), "ZN: dense rank + winsor rows");
+  __shared__ int32_t zn_sch[ZN ? PW_LDS_MAX : 1];
+  __shared__ double zn_nodes[ZN ? FR_ZN_NODES : 1];
+  __shared__ int zn_iscr[ZN ? NW + 2 : 1];
   FrIcRow rw{};
   __shared__ int ic_ne[2];                    // E-list lengths (IC)
   if constexpr (IC) {
@@ -403,6 +422,44 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     hmax = ok ? max(hmax, h) : hmax;
     wv += __popcll(__ballot(ok));
     if (PRES) wp += __popcll(__ballot(p));
+    if constexpr (ZN)
+      if (in) reinterpret_cast<double*>(lds)[fr_opaque(t) + k * NT] = v;   // the row for the moments
+  }
+  if constexpr (ZN) {
+    // cs_zscore / market_neutralize: numpy nanmean and nanvar (ddof 0) by the pairwise
+    // schedule of n = A (NaN -> 0 in the sums, counted apart), as k_cs_moment_rg
+    const double* vrow = reinterpret_cast<const double*>(lds);
+    const int32_t* g = zn.pw.get(An);
+    const bool sl = zn.slen <= PW_LDS_MAX;
+    if (sl)
+      for (int i = t; i < zn.slen; i += NT) zn_sch[i] = g[i];
+    __syncthreads();
+    const int32_t* sch = sl ? zn_sch : g;
+    int cnt, c2;
+    const double s1 = block_pw_sum_w0<NT>([&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; },
+                                          [&](int i) { return (int)(vrow[i] == vrow[i]); }, sch, zn_nodes,
+                                          zn_iscr, &cnt);
+    const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+    const double s2 = block_pw_sum_w0<NT>([&](int i) {
+      const double u = vrow[i];
+      const double z = u == u ? u : 0.0;
+      const double q = (mean - z) * (mean - z);
+      return u == u ? q : 0.0;
+    }, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
+    const double var = cnt > 0 ? s2 / (double)cnt : qnan();
+    const double sd = sqrt(var);
+    const bool g2 = sd == 0.0 || sd != sd;     // neutralize: sigma in {0, NaN} -> 0
+    double* yz = zn.Yz + row * ld;
+    double* yn = zn.Yn + row * ld;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      if (!fr_in<NT>(t, k, (int)A)) continue;
+      const int ia = fr_opaque(t) + k * NT;
+      const double o = (vrow[ia] - mean) / sd;
+      __builtin_nontemporal_store(o, yz + ia);
+      __builtin_nontemporal_store(g2 ? 0.0 : o, yn + ia);
+    }
+    __syncthreads();                          // every read of the staged row is done
   }
   fr_park_sample<NT, EMAX>(tab, key);
 #pragma unroll

@@ -462,11 +462,12 @@ fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const d
   FMX_LAUNCH_CHECK("k_ic_empty");
   FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
   FrIc ic{R, nanb, rsh, F, nw, L0, L1, NL, out, ovf, RK};
+  FrZn zn{};
   int method = FMX_RANK_AVERAGE;
   const uint8_t* present = nullptr;
   fmx_rank2_t* RKrow = nullptr;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic};
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic, (void*)&zn};
   if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
   static const int list_grid = [] {

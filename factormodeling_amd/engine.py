@@ -234,6 +234,28 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
     return Yr, Yw
 
 
+def cs_rank_winsor_zn(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, out_zscore=None, out_neutralize=None,
+                      rank2=None):
+    """cs_rank(average), cs_winsor(qlo, qhi), cs_zscore and market_neutralize of the same
+    dense rows in one pass (fmx_cs_rank_winsor_zn: each row read once); every output is
+    bit-identical to its own kernel.  ``rank2``: also the doubled ranks (as cs_rank_winsor).
+    Returns (Yrank, Ywinsor, Yzscore, Yneutralize)."""
+    X = as3(X)
+    _check_panel(X)
+    F, D, A = X.shape
+    outs = [_out(X, o) for o in (out_rank, out_winsor, out_zscore, out_neutralize)]
+    if rank2 is not None:
+        if rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
+            raise _lib.FmxError("rank2 must be a contiguous int16 (bit pattern uint16) [F][D][A] tensor")
+    if A > FINE_RANK_MAX_A and rank2 is None:
+        cs_rank_winsor(X, qlo, qhi, outs[0], outs[1])
+        cs_zscore_neutralize(X, outs[2], outs[3])
+        return tuple(outs)
+    call("fmx_cs_rank_winsor_zn", ptr(X), *[ptr(o) for o in outs], F, D, A, A, float(qlo), float(qhi), ptr(rank2),
+         stream_ptr())
+    return tuple(outs)
+
+
 def cs_rank_winsor_ic(X, R, lags=(1, 2), qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, ranks_only=False,
                       rank2=None):
     """cs_rank(average) + cs_winsor(qlo, qhi) and the daily IC records of the same rows in

@@ -94,13 +94,18 @@ def _op_key(kind, op, w):
     return f"{kind}:{op or ''}:{w or ''}"
 
 
-def plan_ops(ops, be, fuse=True):
+def plan_ops(ops, be, fuse=True, zn=True):
     """Group the operator list into launches.  With ``fuse`` and a backend that has the
     multi-output kernels: the rolling set {mean, std, zscore, decay at W; rank at WR}
     becomes one ts_set pass, cs_zscore + market_neutralize one moment pass, cs_rank +
-    cs_winsor one histogram pass.  Returns [(stage_name, [(kind, op, w), ...])]."""
+    cs_winsor one histogram pass -- and with ``zn`` all four cross-sectional operators one
+    pass over the rows (cs_rank_winsor_zn: the row is read once).  Returns
+    [(stage_name, [(kind, op, w), ...])]."""
     left = list(ops)
     stages = []
+    quad = [("cs_rank", None, None), ("winsor", None, None), ("cs", "zscore", None), ("cs", "market_neutralize", None)]
+    fuse_zn = (fuse and zn and hasattr(be, "cs_rank_winsor_zn") and not getattr(be, "fused_ic", False)
+               and all(p in left for p in quad))
     if fuse and hasattr(be, "ts_set"):
         ts = [o for o in left if o[0] == "ts" and o[1] in ("mean", "std", "zscore", "rank", "decay")]
         W = {o[2] for o in ts if o[1] != "rank"}
@@ -111,12 +116,17 @@ def plan_ops(ops, be, fuse=True):
             wr = next(iter(WR)) if WR else w
             stages.append((f"ts_set:{w}:{wr}", ts))
             left = [o for o in left if o not in ts]
+    if fuse_zn:
+        left = [o for o in left if o not in quad]
     if fuse and hasattr(be, "cs_rank_winsor"):
         pair = [("cs_rank", None, None), ("winsor", None, None)]
         if all(p in left for p in pair):
             stages.append(("cs_rank_winsor", pair))
             left = [o for o in left if o not in pair]
     stages += [(_op_key(*o), [o]) for o in left]
+    if fuse_zn:
+        # last: its cs_zscore output is still in its buffer when the Gram reads it
+        return stages + [("cs_rank_winsor_zn", quad)]
     if fuse and hasattr(be, "cs_zscore_neutralize"):
         # last: its cs_zscore output is still in its buffer when the Gram reads it
         pair = [("cs", "zscore", None), ("cs", "market_neutralize", None)]
@@ -289,6 +299,11 @@ class EngineBackend:
         """``rank2``: also the doubled ranks the daily IC starts from."""
         E.cs_rank_winsor(X, 0.01, 0.99, outs[0], outs[1], rank2=rank2)
 
+    @staticmethod
+    def cs_rank_winsor_zn(X, outs, rank2=None):
+        """cs_rank, cs_winsor, cs_zscore and market_neutralize of the rows in one pass."""
+        E.cs_rank_winsor_zn(X, 0.01, 0.99, *outs, rank2=rank2)
+
     ranked_ic_max_a = E.RANKED_IC_MAX_A
 
     # ranks-only pass + wave IC vs the standalone IC kernel at C5's 10,000 assets:
@@ -386,6 +401,11 @@ class EngineBackend:
 ENGINE = EngineBackend()
 
 
+# the per-date stages a step runs while the halo exchange is in flight (their owned-date
+# results read no halo row); the Gram follows them on its z-score
+EARLY_STAGES = ("cs_zscore_neutralize", "cs_rank_winsor_zn")
+
+
 def _stage_stream(name, streams):
     """The stream a planned stage runs on (None: the current stream).  Three independent
     chains of the step: the rolling set (streams[0]); cs_zscore + market_neutralize, whose
@@ -410,7 +430,7 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     owned-date output (tests only); ``side`` (a dict) receives by-products later stages
     reuse (cs_zscore's row stats; "rank2", the doubled ranks of X, written into
     side["rank2_buf"] when it fits).  ``only``: run just the stages it accepts (by name)."""
-    stages = plan_ops(cfg.ops, be, cfg.fuse)
+    stages = plan_ops(cfg.ops, be, cfg.fuse, zn=not streams and not cfg.streams)
     offs, need = [], 0
     for _, ops in stages:
         offs.append(need if streams else 0)
@@ -441,6 +461,17 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
         if side is not None:
             side["stats"] = st
             side["zscore"] = outs[0]                # the Gram's z (valid until the buffer is reused)
+    elif name == "cs_rank_winsor_zn":
+        rk = None
+        if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
+            rk = side.get("rank2_buf")
+            if rk is None or tuple(rk.shape) != tuple(X.shape):
+                rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=X.device)
+            side["rank2"] = rk
+        be.cs_rank_winsor_zn(X, outs, rank2=rk)
+        if side is not None:
+            side["stats"] = None
+            side["zscore"] = outs[2]                # the Gram's z (valid until the buffer is reused)
     elif name == "cs_rank_winsor":
         if side is not None and X.shape[2] <= getattr(be, "ranked_ic_max_a", 0):
             # the ranks of X also feed the daily IC (no second ranking of the panel)
@@ -554,6 +585,12 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     side = {"rank2_buf": getattr(sp, "rank2", None), "R": sp.R, "lags": tuple(cfg.ic_lags)}
     streams = None
     early = not cfg.streams
+    # the fused cross-sectional pass also writes the ranks of the halo rows, which the first
+    # owned dates' daily IC reads (exposure date = target date - lag): with a halo it runs
+    # after the exchange lands, and the Gram (on its z-score) after it
+    zn_plan = any(n == "cs_rank_winsor_zn" for n, _ in plan_ops(cfg.ops, be, cfg.fuse, zn=not cfg.streams))
+    zn_late = zn_plan and sp.world > 1
+    early_names = tuple(n for n in EARLY_STAGES if not (zn_late and n == "cs_rank_winsor_zn"))
     t0 = _ev(timers)
     halo = sp.exchange_halo_start()
     _rec(timers, "halo", t0)
@@ -565,8 +602,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         # not owned (stale until the exchange lands: the same data every step).
         if cfg.ops:
             sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                              own=slice(sp.halo, None), side=side, only=lambda n: n == "cs_zscore_neutralize")
-        if cfg.gram and hasattr(be, "corr_gram"):
+                              own=slice(sp.halo, None), side=side, only=lambda n: n in early_names)
+        if cfg.gram and hasattr(be, "corr_gram") and not zn_late:
             t0 = _ev(timers)
             GN = gram_partials(sp, be, side)
             _rec(timers, "gram", t0)
@@ -585,7 +622,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if cfg.ops:
         sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
                           own=slice(sp.halo, None), side=side, streams=streams,
-                          only=(lambda n: n != "cs_zscore_neutralize") if early else None)
+                          only=(lambda n: n not in early_names) if early else None)
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)
@@ -663,7 +700,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if cfg.gram:
         # correlation Gram over owned dates, summed over ranks in rank order
         t0 = _ev(timers)
-        if GN is not None:
+        made = GN is not None
+        if made:
             for T in GN[1]:                       # made on streams[1]: now used on this one
                 if T.is_cuda:
                     T.record_stream(torch.cuda.current_stream(T.device))
@@ -671,7 +709,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
             GN = gram_partials(sp, be, side)
         G, N = gram_total(sp, be, GN)
         C = torch.where(N > 0, G / N.clamp_min(1.0), torch.zeros_like(G))
-        _rec(timers, "gram_sum" if GN is not None else "gram", t0)
+        _rec(timers, "gram_sum" if made else "gram", t0)
         t0 = _ev(timers)
         rir = summ[0, :, 3]
         full_order = torch.argsort(torch.nan_to_num(rir, nan=-np.inf), descending=True, stable=True)

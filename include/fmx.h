@@ -171,6 +171,14 @@ fmx_status fmx_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t
 fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double* Ywinsor, int64_t F, int64_t D, int64_t A,
                               int64_t ld, double qlo, double qhi, const uint8_t* present, fmx_rank2_t* rank2,
                               void* stream);
+/* cs_rank (average) + cs_winsor (qlo, qhi) + cs_zscore + market_neutralize of the same dense
+ * rows in ONE pass (operations.py:54-68, :77-78, :171-182): each row is read once for the
+ * four operators; every output is bit-identical to its own entry point (fmx_cs_rank_winsor,
+ * fmx_cs_zscore_neutralize); rank2 as in fmx_cs_rank_winsor (or NULL).  Five distinct
+ * panels.  Rows past the fused kernel (A > 16384) take the two two-output passes. */
+fmx_status fmx_cs_rank_winsor_zn(const double* X, double* Yrank, double* Ywinsor, double* Yzscore, double* Yneutralize,
+                                 int64_t F, int64_t D, int64_t A, int64_t ld, double qlo, double qhi,
+                                 fmx_rank2_t* rank2, void* stream);
 /* cs_rank, every method, for any row length (A <= 65535): rows sorted in HBM (rocPRIM
  * segmented radix sort of (value key, asset) pairs, stable), then one wave per row walks
  * its tie runs and scatters the ranks.  fmx_cs_rank takes 'first' / 'dense' up to A = 8192

@@ -112,9 +112,30 @@ def test_cs_fused_ragged(dev):
 def test_plan_ops_groups_the_c2_set():
     from factormodeling_amd import pipeline as PL
     stages = PL.plan_ops(PL.OPS, PL.ENGINE, True)
+    assert [s for s, _ in stages] == ["ts_set:20:10", "cs_rank_winsor_zn"]
+    assert sorted(o for _, ops in stages for o in ops) == sorted(PL.OPS)
+    stages = PL.plan_ops(PL.OPS, PL.ENGINE, True, zn=False)
     assert [s for s, _ in stages] == ["ts_set:20:10", "cs_rank_winsor", "cs_zscore_neutralize"]
     assert sorted(o for _, ops in stages for o in ops) == sorted(PL.OPS)
     assert len(PL.plan_ops(PL.OPS, PL.ENGINE, False)) == len(PL.OPS)
+
+
+@pytest.mark.parametrize("A", [9, 700, 3500, 5000, 10000, 13000])
+def test_cs_rank_winsor_zn_matches_separate_passes(dev, A):
+    """The four cross-sectional operators in one pass (fmx_cs_rank_winsor_zn) equal the two
+    two-output passes bit for bit, the doubled ranks included: empty, constant, < 5-valid and
+    single-valid rows, ties, rows whose EMAX is rounded up."""
+    import torch
+    import factormodeling_amd.engine as E
+    X = torch.as_tensor(_cs_panel(A, 3, 9, A), device=dev)
+    rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
+    Yr, Yw, Yz, Yn = E.cs_rank_winsor_zn(X, 0.01, 0.99, rank2=rk)
+    rk_ref = torch.empty_like(rk)
+    Rr, Rw = E.cs_rank_winsor(X, 0.01, 0.99, rank2=rk_ref)
+    Rz, Rn = E.cs_zscore_neutralize(X)
+    for got, ref, what in ((Yr, Rr, "rank"), (Yw, Rw, "winsor"), (Yz, Rz, "zscore"), (Yn, Rn, "neutralize")):
+        assert np.array_equal(got.cpu().numpy(), ref.cpu().numpy(), equal_nan=True), what
+    assert torch.equal(rk, rk_ref)
 
 
 def _ic_case(seed, F, D, A, r_nan, x_nan=0.02):

@@ -111,6 +111,8 @@ OPS = {
     "cs_zn": (lambda X, R, Y: E.cs_zscore_neutralize(X, Y, _set_outs(X)["mean"]), 24),
     "cs_rw": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"]), 24),
     "cs_rw_rk": (lambda X, R, Y: E.cs_rank_winsor(X, 0.01, 0.99, Y, _set_outs(X)["mean"], rank2=_rank2(X)), 26),
+    "cs_rwzn_rk": (lambda X, R, Y: E.cs_rank_winsor_zn(X, 0.01, 0.99, Y, _set_outs(X)["mean"], _set_outs(X)["std"],
+                                                      _set_outs(X)["zscore"], rank2=_rank2(X)), 42),
     "ic_ranked": (lambda X, R, Y: E.ic_daily(X, R, (1, 2), rank2=_rank2(X)), 10),
     "cs_rw_ic": (lambda X, R, Y: E.cs_rank_winsor_ic(X, R, (1, 2), 0.01, 0.99, Y, _set_outs(X)["mean"],
                                                      rank2=_RK.setdefault("rk", torch.empty(X.shape, dtype=E.RANK2_DTYPE,
