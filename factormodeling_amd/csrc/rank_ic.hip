@@ -236,7 +236,7 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   double ax[2] = {0.0, 0.0}, ar[2] = {0.0, 0.0};
   bool ref[2] = {false, false};
   int cnt[2] = {0, 0};
-  uint32_t dif = 0;                           // bit 2m: an x differs from lag m's reference, 2m+1: an r
+  uint64_t dm[4] = {0, 0, 0, 0};              // [2m]: lanes whose x differed from lag m's reference, [2m+1]: r
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -268,6 +268,9 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
         ar[m] = fr_readlane_d(r[m], l);
         ref[m] = true;
       }
+      // difference flags as wave masks, in wave-uniform control flow (scalar ORs)
+      dm[2 * m] |= __ballot(p && x != ax[m]);
+      dm[2 * m + 1] |= __ballot(p && r[m] != ar[m]);
       if (!p) continue;
       int corr = 0;
       if (ne[m]) {
@@ -281,11 +284,14 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
       }
       const uint32_t k2 = rk - (uint32_t)corr;
       const double dx = x - ax[m], dy = r[m] - ar[m];
-      dif |= ((x != ax[m]) ? 1u : 0u) << (2 * m);
-      dif |= ((r[m] != ar[m]) ? 1u : 0u) << (2 * m + 1);
+      // the moment sums with fused multiply-adds: the records are tolerance-pinned (single-pass
+      // moments about the first pair, ~1e-15 relative), not bit-pinned, and an fma per term is
+      // both one instruction and one rounding fewer
       sm[m][0] += dx; sm[m][1] += dy;
-      sm[m][2] += dx * dx; sm[m][3] += dy * dy; sm[m][4] += dx * dy;
-      sm[m][5] += (double)k2 * dy;
+      sm[m][2] = __builtin_fma(dx, dx, sm[m][2]);
+      sm[m][3] = __builtin_fma(dy, dy, sm[m][3]);
+      sm[m][4] = __builtin_fma(dx, dy, sm[m][4]);
+      sm[m][5] = __builtin_fma((double)k2, dy, sm[m][5]);
       kk[m] += (uint64_t)k2 * k2;
     }
   }
@@ -303,7 +309,7 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   }
   uint32_t dflags = 0;                        // wave OR of the difference bits
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dflags |= (__ballot((dif >> q) & 1) != 0 ? 1u : 0u) << q;
+  for (int q = 0; q < 4; ++q) dflags |= (dm[q] != 0 ? 1u : 0u) << q;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (lane == 0) {
