@@ -421,7 +421,7 @@ def _stage_stream(name, streams):
 
 
 def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None, own=slice(None), side=None,
-            streams=None, only=None):
+            streams=None, only=None, zn=True):
     """Operator set over the local panel (halo rows included as warm-up), as planned by
     ``plan_ops``; every operator writes its own output buffer (``bufs``: a list of tensors
     shaped like X, reused across steps).  Sequentially, stages share the buffers (as many
@@ -430,7 +430,7 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     owned-date output (tests only); ``side`` (a dict) receives by-products later stages
     reuse (cs_zscore's row stats; "rank2", the doubled ranks of X, written into
     side["rank2_buf"] when it fits).  ``only``: run just the stages it accepts (by name)."""
-    stages = plan_ops(cfg.ops, be, cfg.fuse, zn=not streams and not cfg.streams)
+    stages = plan_ops(cfg.ops, be, cfg.fuse, zn=zn and not streams and not cfg.streams)
     offs, need = [], 0
     for _, ops in stages:
         offs.append(need if streams else 0)
@@ -585,12 +585,13 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     side = {"rank2_buf": getattr(sp, "rank2", None), "R": sp.R, "lags": tuple(cfg.ic_lags)}
     streams = None
     early = not cfg.streams
-    # the fused cross-sectional pass also writes the ranks of the halo rows, which the first
-    # owned dates' daily IC reads (exposure date = target date - lag): with a halo it runs
-    # after the exchange lands, and the Gram (on its z-score) after it
-    zn_plan = any(n == "cs_rank_winsor_zn" for n, _ in plan_ops(cfg.ops, be, cfg.fuse, zn=not cfg.streams))
-    zn_late = zn_plan and sp.world > 1
-    early_names = tuple(n for n in EARLY_STAGES if not (zn_late and n == "cs_rank_winsor_zn"))
+    # the four cross-sectional operators in one pass only without date shards: that pass also
+    # ranks the halo rows, which the first owned dates' daily IC reads (exposure date = target
+    # date - lag), so sharded it would have to wait for the halo exchange; the two-pass form
+    # keeps cs_zscore + neutralize and the Gram in front of the exchange (§7), which costs
+    # less per shard than an exposed exchange
+    zn = sp.world == 1
+    early_names = EARLY_STAGES
     t0 = _ev(timers)
     halo = sp.exchange_halo_start()
     _rec(timers, "halo", t0)
@@ -602,8 +603,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         # not owned (stale until the exchange lands: the same data every step).
         if cfg.ops:
             sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                              own=slice(sp.halo, None), side=side, only=lambda n: n in early_names)
-        if cfg.gram and hasattr(be, "corr_gram") and not zn_late:
+                              own=slice(sp.halo, None), side=side, only=lambda n: n in early_names, zn=zn)
+        if cfg.gram and hasattr(be, "corr_gram"):
             t0 = _ev(timers)
             GN = gram_partials(sp, be, side)
             _rec(timers, "gram", t0)
@@ -622,7 +623,7 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if cfg.ops:
         sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
                           own=slice(sp.halo, None), side=side, streams=streams,
-                          only=(lambda n: n not in early_names) if early else None)
+                          only=(lambda n: n not in early_names) if early else None, zn=zn)
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)
