@@ -1243,6 +1243,10 @@ k_valid_bits(const double* __restrict__ X, const double* __restrict__ stats, int
 // load -> stage -> barrier chain, not by MFMA (skipping the below-diagonal blocks' MFMAs
 // changed nothing) nor by HBM bandwidth.  Tile (bi, bj) covers rows [256 bi, +256),
 // columns [128 bj, +128) for bj >= 2 bi: every (i <= j) pair lies in exactly one tile.
+#ifndef GW_DIAG
+#define GW_DIAG 0      // diagnostics (libfmx_d*.so only): 1 no panel loads, 2 no MFMAs, 3 no chunk barrier,
+                       // 4 no z-score arithmetic while staging
+#endif
 constexpr int GW_I = 256, GW_J = 128, GW_K = 16, GW_KP = GW_K + 2;   // row pitch 36 dwords: conflict-free b64
 constexpr size_t GRAM_W_LDS = sizeof(double) * 2 * (GW_I + GW_J) * GW_KP;
 __host__ __device__ inline int64_t gw_ntile(int64_t F) {
@@ -1309,33 +1313,51 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   const int64_t nchunk = (de - ds) * nch;
   double ra[4], rb[2];
   double2 sa, sb;                             // (mean, sd) of the staged rows' date
-  auto issue = [&](int64_t c) {
-    const int64_t d = ds + c / nch, a0 = (c % nch) * GW_K;
-    const double* pa = X + ((int64_t)(i0 + ar) * D + d) * ld + a0 + ac;
-    const double* pb = X + ((int64_t)(j0 + br) * D + d) * ld + a0 + bc;
-    if (VEC && rowA && a0 + ac + 4 <= A) {
+  // chunk cursors (wave-uniform) of the next issue and the next stage: chunks are issued and
+  // staged in order, so (date, asset offset) advance by steps -- the c / nch, c % nch of a
+  // 64-bit chunk index cost two long VALU division sequences per chunk
+  int is_d = (int)ds, st_dr = (int)(ds - d0), st_j = 0, is_a = 0;
+  const int nch32 = (int)nch;
+  auto issue = [&](int64_t) {
+    const int64_t d = is_d;
+    const int a0 = is_a, A32 = (int)A;
+    is_a += GW_K;
+    if (is_a >= A) { is_a = 0; ++is_d; }
+#if GW_DIAG == 1
+    ra[0] = ra[1] = ra[2] = ra[3] = (double)(a0 & 7); rb[0] = rb[1] = (double)(d & 3);
+    sa = make_double2(0.5, 1.0); sb = sa;
+    return;
+#endif
+    // the row indices pass through an empty asm: the 64-bit row bases are recomputed per
+    // chunk instead of being hoisted out of the chunk loop (their VGPRs would spill, and a
+    // scratch reload waits on the prefetched chunk's loads)
+    int rA = i0 + ar, rB = j0 + br;
+    asm volatile("" : "+v"(rA), "+v"(rB));
+    const double* pa = X + ((int64_t)rA * D + d) * ld + a0 + ac;
+    const double* pb = X + ((int64_t)rB * D + d) * ld + a0 + bc;
+    if (VEC && rowA && a0 + ac + 4 <= A32) {
       const dbl2 u = reinterpret_cast<const dbl2*>(pa)[0], v = reinterpret_cast<const dbl2*>(pa)[1];
       ra[0] = u[0]; ra[1] = u[1]; ra[2] = v[0]; ra[3] = v[1];
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = (rowA && a0 + ac + q < A) ? pa[q] : qnan();
+      for (int q = 0; q < 4; ++q) ra[q] = (rowA && a0 + ac + q < A32) ? pa[q] : qnan();
     }
-    if (VEC && rowB && a0 + bc + 2 <= A) {
+    if (VEC && rowB && a0 + bc + 2 <= A32) {
       const dbl2 u = reinterpret_cast<const dbl2*>(pb)[0];
       rb[0] = u[0]; rb[1] = u[1];
     } else {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) rb[q] = (rowB && a0 + bc + q < A) ? pb[q] : qnan();
+      for (int q = 0; q < 2; ++q) rb[q] = (rowB && a0 + bc + q < A32) ? pb[q] : qnan();
     }
     const double2* z = reinterpret_cast<const double2*>(zst);   // [F][D] (mean, 1/sd or 0)
-    sa = rowA ? z[(int64_t)(i0 + ar) * D + d] : make_double2(0.0, 0.0);
-    sb = rowB ? z[(int64_t)(j0 + br) * D + d] : make_double2(0.0, 0.0);
+    sa = rowA ? z[(int64_t)rA * D + d] : make_double2(0.0, 0.0);
+    sb = rowB ? z[(int64_t)rB * D + d] : make_double2(0.0, 0.0);
   };
   // validity bits: the diagonal tiles (bj = 2 bi, whose i-rows cover every row once per
   // date) write them while staging -- half-word (16 assets) per row and chunk, in the
   // factor-major [F][nd][2 nwd] u16 = [F][nd][nwd] u32 layout k_gram_popc_fm reads
   const bool wbits = bits16 != nullptr && bj == 2 * bi;
-  auto stage = [&](int buf, int64_t c) {
+  auto stage = [&](int buf, int64_t) {
     double* As = gsm + buf * BUF;
     double* Bs = As + GW_I * GW_KP;
     const bool oka = sa.y > 0.0, okb = sb.y > 0.0;           // 1/sd > 0 <=> sd > 0
@@ -1348,15 +1370,22 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
         const uint64_t m = __ballot(rowA && oka && ra[q] == ra[q]);
         hw |= (uint32_t)((m >> (lane & ~3)) & 0xfu) << (4 * q);
       }
-      if ((lane & 3) == 0 && rowA) {
-        const int64_t dr = (ds - d0) + c / nch, j = c - (c / nch) * nch;
-        bits16[((int64_t)(i0 + ar) * (d1 - d0) + dr) * (2 * nwd) + j] = (uint16_t)hw;
-      }
+      int rA = i0 + ar;
+      asm volatile("" : "+v"(rA));                           // not hoisted: see issue()
+      if ((lane & 3) == 0 && rowA) bits16[((int64_t)rA * (d1 - d0) + st_dr) * (2 * nwd) + st_j] = (uint16_t)hw;
     }
+    if (++st_j == nch32) { st_j = 0; ++st_dr; }
+#if GW_DIAG == 4
+#pragma unroll
+    for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = ra[q];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = rb[q];
+#else
 #pragma unroll
     for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = (oka && ra[q] == ra[q]) ? (ra[q] - sa.x) * sa.y : 0.0;
 #pragma unroll
     for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = (okb && rb[q] == rb[q]) ? (rb[q] - sb.x) * sb.y : 0.0;
+#endif
   };
   auto mfma_chunk = [&](int buf) {
     const double* As = gsm + buf * BUF;
@@ -1373,8 +1402,13 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n)
-          if ((live >> (m * 2 + n)) & 1u)
+          if ((live >> (m * 2 + n)) & 1u) {
+#if GW_DIAG == 2
+            acc[m][n][0] += af[m] * bf[n];
+#else
             acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+#endif
+          }
       // one k-step's fragments live at a time (the next step's reads are not hoisted over
       // these MFMAs): 128 VGPRs at four waves per SIMD without spilling
       __builtin_amdgcn_sched_barrier(0);
@@ -1400,7 +1434,11 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
     if (stage_first) next();
     mfma_chunk((int)(c & 1));
     if (!stage_first) next();
+#if GW_DIAG == 3
+    if (c < 2) __syncthreads();
+#else
     __syncthreads();
+#endif
   }
   double* p = part + (slice * ntile + tile) * (GW_I * GW_J);
 #pragma unroll
@@ -1494,6 +1532,93 @@ k_gram_popc_fm(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t
     }
 }
 
+// N = M M^T on the i8 matrix cores (v_mfma_i32_16x16x64_i8): the validity bits expand to 0/1
+// bytes in registers, so the pair counts of a 64-bit K-step cost one MFMA per 16 x 16 block
+// instead of 2 x 256 AND / popcounts.  128 x 128 upper tiles (incl. the diagonal) of 4 waves
+// as 2 x 2, each a 64 x 64 sub-tile of 4 x 4 MFMAs (64 i32 accumulators per lane); chunks of
+// 16 words per row staged in LDS.  Fragment map: lane (r = l & 15, g = l >> 4) of K-step s
+// takes word 2s + (g >> 1) of its row, shifted by 4 (g & 1); dword q of its 16 operand bytes
+// is (w >> q) & 0x01010101.  A and B lanes of one group hold the same k set on the MFMA's
+// mirrored A / B maps, so every bit position meets its own in the other row exactly once
+// whatever the hardware's k order within a group.  C/D: col = l & 15, row = 4 (l >> 4) + q.
+constexpr int GC_T = 128, GC_KW = 16, GC_LP = 20;          // tile, words per chunk, LDS pitch
+typedef int gc_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ gc_v4i gc_expand(uint32_t t) {
+  constexpr uint32_t M = 0x01010101u;
+  gc_v4i d;
+  d[0] = (int)(t & M);
+  d[1] = (int)((t >> 1) & M);
+  d[2] = (int)((t >> 2) & M);
+  d[3] = (int)((t >> 3) & M);
+  return d;
+}
+template <bool VEC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_gram_cnt_i8(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t wps,
+              unsigned long long* __restrict__ ncnt) {
+  __shared__ uint32_t Ls[2 * GC_T * GC_LP];                   // rows 0..127: I tile, 128..255: J
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int tt = blockIdx.x, ti = 0;
+  const int T = (int)((F + GC_T - 1) / GC_T);
+  while (tt >= T - ti) { tt -= T - ti; ++ti; }
+  const int I0 = ti * GC_T, J0 = (ti + tt) * GC_T;
+  const int64_t w0 = (int64_t)blockIdx.y * wps, w1 = min<int64_t>(nw, w0 + wps);
+  const int wr = wid >> 1, wc = wid & 1, r = lane & 15, g = lane >> 4;
+  const int hw = g >> 1, sh = 4 * (g & 1);
+  gc_v4i acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = gc_v4i{0, 0, 0, 0};
+  // loader: thread t stages words 4 (t & 3) .. +3 of rows (t >> 2) + 64 i, i = 0..3
+  const int lr = tid >> 2, lw = (tid & 3) * 4;
+  for (int64_t wc0 = w0; wc0 < w1; wc0 += GC_KW) {
+    uint32_t v[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = lr + 64 * i;
+      const int64_t fr = row < GC_T ? I0 + row : J0 + row - GC_T;
+      const uint32_t* p = bits + fr * nw + wc0 + lw;
+      const bool ok = fr < F;
+      if (VEC && ok && wc0 + lw + 4 <= w1) {
+        const uint4 u = *reinterpret_cast<const uint4*>(p);
+        v[i][0] = u.x; v[i][1] = u.y; v[i][2] = u.z; v[i][3] = u.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[i][q] = (ok && wc0 + lw + q < w1) ? p[q] : 0u;
+      }
+    }
+    __syncthreads();                                          // the previous chunk's reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint4*>(&Ls[(lr + 64 * i) * GC_LP + lw]) = make_uint4(v[i][0], v[i][1], v[i][2], v[i][3]);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < GC_KW / 2; ++s) {
+      gc_v4i a[4], b[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = gc_expand(Ls[(wr * 64 + m * 16 + r) * GC_LP + 2 * s + hw] >> sh);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) b[n] = gc_expand(Ls[(GC_T + wc * 64 + n * 16 + r) * GC_LP + 2 * s + hw] >> sh);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[m], b[n], acc[m][n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);                      // one K-step's fragments live at a time
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gi = I0 + wr * 64 + m * 16 + 4 * g + q, gj = J0 + wc * 64 + n * 16 + r;
+        const int c = acc[m][n][q];
+        if (gi < F && gj < F && gi <= gj && c) atomicAdd(&ncnt[(int64_t)gi * F + gj], (unsigned long long)c);
+      }
+}
+
 // N from the counts (upper triangle incl. the diagonal), mirrored; accumulate adds to N
 __global__ void k_gram_counts(const unsigned long long* __restrict__ ncnt, int64_t F, double* __restrict__ N,
                               int accumulate) {
@@ -1579,6 +1704,42 @@ static DirectPlan direct_plan(int64_t F, int64_t D, int64_t A, int64_t d0, int64
   return p;
 }
 
+// N = M M^T of the validity bits [F][nw] into ncnt (zeroed by the caller): the i8-MFMA tile
+// kernel, or (FMX_GRAM_CNT=0, the A/B arm) the AND / popcount kernel
+static fmx_status launch_pair_counts(const uint32_t* bits, int64_t F, int64_t nw, unsigned long long* ncnt,
+                                     hipStream_t st) {
+  static const int mode = [] { const char* e = getenv("FMX_GRAM_CNT"); return e ? atoi(e) : 1; }();
+  if (mode == 0) {
+    const int T = (int)ceil_div(F, (int64_t)PF_T);
+    const int ntp = T * (T + 1) / 2;
+    // >= ~2048 workgroups: the word range is cut into pieces of whole 64-word chunks
+    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PF_W), 2048 / ntp + 1));
+    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PF_W) * PF_W;
+    k_gram_popc_fm<<<dim3((unsigned)ntp, (unsigned)ceil_div(nw, wps)), 256, 0, st>>>(bits, F, nw, wps, ncnt);
+    FMX_LAUNCH_CHECK("k_gram_popc_fm");
+    return FMX_OK;
+  }
+  const int T = (int)ceil_div(F, (int64_t)GC_T);
+  const int64_t ntp = (int64_t)T * (T + 1) / 2;
+  // word slices: ~2 rounds of 4 workgroups per CU with a full last round, whole 16-word
+  // chunks, and at most 2^25 words per slice (i32 accumulators: <= 32 bits per word)
+  const int64_t nchunk = ceil_div(nw, (int64_t)GC_KW);
+  int64_t nks = 1;
+  double best = -1.0;
+  for (int64_t k = 1; k <= std::min<int64_t>(nchunk, std::max<int64_t>(1, 4096 / ntp)); ++k) {
+    const int64_t wg = ntp * k, slots = 1024;
+    const double eff = (double)wg / (double)(ceil_div(wg, slots) * slots) - (wg < slots ? 1.0 : 0.0);
+    if (eff > best + 0.01) { best = eff; nks = k; }
+  }
+  nks = std::max<int64_t>(nks, ceil_div(nw, (int64_t)1 << 25));
+  const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)GC_KW) * GC_KW;
+  const dim3 grid((unsigned)ntp, (unsigned)ceil_div(nw, wps));
+  if (nw % 4 == 0) k_gram_cnt_i8<true><<<grid, 256, 0, st>>>(bits, F, nw, wps, ncnt);
+  else k_gram_cnt_i8<false><<<grid, 256, 0, st>>>(bits, F, nw, wps, ncnt);
+  FMX_LAUNCH_CHECK("k_gram_cnt_i8");
+  return FMX_OK;
+}
+
 extern "C" int64_t fmx_gram_direct_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1) {
   if (F <= 0 || d1 <= d0) return 0;
   return direct_plan(F, D, A, d0, d1).bytes();
@@ -1627,13 +1788,7 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
                                                                                  G, accumulate);
   FMX_LAUNCH_CHECK("k_gram_reduce_w");
   FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
-  const int T = (int)ceil_div(F, (int64_t)PF_T);
-  const int ntp = T * (T + 1) / 2;
-  // >= ~2048 workgroups: the word range is cut into pieces of whole 64-word chunks
-  const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(pl.nw, (int64_t)4 * PF_W), 2048 / ntp + 1));
-  const int64_t wps = ceil_div(ceil_div(pl.nw, nks), (int64_t)PF_W) * PF_W;
-  k_gram_popc_fm<<<dim3((unsigned)ntp, (unsigned)ceil_div(pl.nw, wps)), 256, 0, st>>>(bits, F, pl.nw, wps, ncnt);
-  FMX_LAUNCH_CHECK("k_gram_popc_fm");
+  if (fmx_status e = launch_pair_counts(bits, F, pl.nw, ncnt, st)) return e;
   k_gram_counts<<<(unsigned)ceil_div(F * F, (int64_t)256), 256, 0, st>>>(ncnt, F, N, accumulate);
   FMX_LAUNCH_CHECK("k_gram_counts");
   return FMX_OK;
@@ -1705,12 +1860,7 @@ extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats
                   (void*)&part, (void*)&bits16, (void*)&nwd};
   FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nwg), dim3(1024), args, GRAM_W_LDS, st));
   FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
-  const int T = (int)ceil_div(F, (int64_t)PF_T);
-  const int ntp = T * (T + 1) / 2;
-  const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(pl.nw, (int64_t)4 * PF_W), 2048 / ntp + 1));
-  const int64_t wps = ceil_div(ceil_div(pl.nw, nks), (int64_t)PF_W) * PF_W;
-  k_gram_popc_fm<<<dim3((unsigned)ntp, (unsigned)ceil_div(pl.nw, wps)), 256, 0, st>>>(bits, F, pl.nw, wps, ncnt);
-  FMX_LAUNCH_CHECK("k_gram_popc_fm");
+  if (fmx_status e = launch_pair_counts(bits, F, pl.nw, ncnt, st)) return e;
   k_gram_fold_w<<<dim3((unsigned)ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, nslice, ntile, F, ncnt, limbs, counts,
                                                                           accumulate ? 1 : 0);
   FMX_LAUNCH_CHECK("k_gram_fold_w");

@@ -580,8 +580,8 @@ def gram_chunked(X, d0=0, d1=None, chunk=None):
 def gram_direct(X, d0=0, d1=None, stats=None):
     """G, N over dates [d0, d1) for wide factor sets (F > 256, C4's 2000) straight from
     the panel (fmx_gram_direct): the z-score (row stats of fmx_cs_moment_stats, computed
-    here unless given) is applied while each tile chunk is staged and N comes from AND +
-    popcount of validity bits -- no Z / M panels in HBM."""
+    here unless given) is applied while each tile chunk is staged and N comes from the
+    validity bits on the i8 matrix cores -- no Z / M panels in HBM."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape

@@ -194,6 +194,29 @@ def test_gram_direct_equals_materialised(dev, F, D, A):
     np.testing.assert_allclose(G2.cpu().numpy(), Zf @ Zf.T, rtol=1e-10, atol=1e-10)
 
 
+@pytest.mark.parametrize("F,D,A", [(300, 40, 700), (129, 33, 1001), (256, 9, 3000)])
+def test_gram_pair_counts_many_word_slices(dev, F, D, A):
+    """N (the pair counts on the i8 matrix cores, k_gram_cnt_i8) over many 16-word chunks
+    and word slices, ragged tile edges (F = 129, 300) and word counts not a multiple of 4:
+    exactly M M^T of the oracle's validity mask (plain and exact Gram entries)."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F * D + A)
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < rng.uniform(0.02, 0.4, size=(F, 1, 1))] = np.nan
+    X[7, 3] = 1.5                                   # constant row
+    X[:, 5, : A // 3] = np.nan                      # a date with a third of the assets missing
+    Xt = torch.as_tensor(X, device=dev)
+    _, M = OG.zscore_exposures(X)
+    Mf = M.reshape(F, -1).astype(np.int64)
+    ref = Mf @ Mf.T
+    _, N1 = E.gram_direct(Xt)
+    assert np.array_equal(N1.cpu().numpy().astype(np.int64), ref)
+    _, N2 = E.gram_direct_exact(Xt)                 # exact partial counts: the upper triangle
+    assert np.array_equal(np.triu(N2.cpu().numpy()), np.triu(ref))
+
+
 def test_corr_prune_selector_through_factor_selector(dev):
     import oracle.metrics as OM
     from factormodeling_amd.factor_selector import FactorSelector
