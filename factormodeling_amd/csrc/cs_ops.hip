@@ -179,17 +179,33 @@ __device__ __forceinline__ double csr_leaf_sum8(double r) {
   r = r + csr_dpp<0x141>(r);    // row_half_mirror: lane 7 - i, the other quad of the 8
   return r;
 }
+// FMX_CS_GRAM_Z (the wide Gram's z pass, fmx_gram_direct_exact): row r of a date chunk
+// (factor r / nd, date d0 + r % nd of X) -> Zc row r (stride apad): z = (x - mean) / sd where
+// x is valid and sd > 0, else 0, and zeros in the pad columns [A, apad); its validity bits
+// (bit a of word a / 32) -> bits row (r / nd) * nd_all + r % nd.
+constexpr int FMX_CS_GRAM_Z = 4;
+struct CsrZc {
+  double* Z;
+  uint32_t* bits;
+  int64_t nd, D, d0, apad, nd_all;
+  int nwd;
+};
+constexpr int CSR_ZC_WORDS = 8 * CSR_EL * (CSR_NT / 8) / 32;   // bit words of the longest row
+
 template <int OP>
-__global__ void __launch_bounds__(CSR_NT, 8)
+__global__ void __launch_bounds__(CSR_NT, OP == FMX_CS_GRAM_Z ? 4 : 8)
 k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
-               PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2, int nts) {
+               PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2, int nts, CsrZc zc) {
   __shared__ int32_t sch[PW_LDS_MAX];
   __shared__ double nodes[2 * (CSR_NT / 8) + 8];
   __shared__ int iscr[CSR_NT / 64 + 2];
+  __shared__ uint32_t bw[OP == FMX_CS_GRAM_Z ? CSR_ZC_WORDS : 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   {
     const int32_t* g = pw.get((int)A);
     for (int i = tid; i < slen; i += CSR_NT) sch[i] = g[i];
+    if (OP == FMX_CS_GRAM_Z)
+      for (int i = tid; i < CSR_ZC_WORDS; i += CSR_NT) bw[i] = 0u;
   }
   __syncthreads();
   PwView sv{sch};
@@ -213,7 +229,7 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
     // than held across the row loop, where it would spill
     const int st = act ? sv.lstart(leaf) : 0, len = act ? sv.llen(leaf) : 0;
     const int stop = len - (len & 7), nfull = stop >> 3;
-    const double* x = X + row * ld;
+    const double* x = X + (OP == FMX_CS_GRAM_Z ? ((row / zc.nd) * zc.D + zc.d0 + row % zc.nd) * ld : row * ld);
     double xv[CSR_EL];
 #pragma unroll
     for (int i = 0; i < CSR_EL; ++i) xv[i] = (i < nfull) ? x[st + j + 8 * i] : 0.0;
@@ -282,7 +298,38 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
       sd = sqrt(var);
     }
     if (stats && tid == 0) { stats[2 * row] = cnt > 0 ? mean : qnan(); stats[2 * row + 1] = cnt > 0 ? sd : qnan(); }
-    if (OP != FMX_CS_STATS_ONLY) {
+    if (OP == FMX_CS_GRAM_Z) {
+      const bool okr = sd > 0.0;                       // cnt > 0 and sigma not 0 (NaN fails)
+      double* zr = zc.Z + row * zc.apad;
+#pragma unroll
+      for (int i = 0; i < CSR_EL; ++i)
+        if (i < nfull) {
+          const double t = xv[i];
+          const bool ok = okr && t == t;
+          zr[st + j + 8 * i] = ok ? (t - mean) / sd : 0.0;
+          // the leaf's 8 lanes hold 8 consecutive assets: one byte of bits, OR-ed in by j == 0
+          const uint32_t byte = (uint32_t)(__ballot(ok) >> (lane & 56)) & 0xffu;
+          if (j == 0 && byte) {
+            const int p = st + 8 * i, w = p >> 5, o = p & 31;
+            atomicOr(&bw[w], byte << o);
+            if (o > 24) atomicOr(&bw[w + 1], byte >> (32 - o));
+          }
+        }
+      if (act && j == 0)
+        for (int q = stop; q < len; ++q) {
+          const double t = x[st + q];
+          const bool ok = okr && t == t;
+          zr[st + q] = ok ? (t - mean) / sd : 0.0;
+          if (ok) atomicOr(&bw[(st + q) >> 5], 1u << ((st + q) & 31));
+        }
+      for (int64_t a = A + tid; a < zc.apad; a += CSR_NT) zr[a] = 0.0;
+      __syncthreads();
+      uint32_t* br = zc.bits + ((row / zc.nd) * zc.nd_all + row % zc.nd) * zc.nwd;
+      for (int w = tid; w < zc.nwd; w += CSR_NT) {
+        br[w] = bw[w];
+        bw[w] = 0u;                                    // the next row's atomics follow the loop-end barrier
+      }
+    } else if (OP != FMX_CS_STATS_ONLY) {
       const bool guard = (OP == FMX_CS_MARKET_NEUTRALIZE) && (sd == 0.0 || sd != sd);
       auto outv = [&](double t) {
         if (OP == FMX_CS_MEAN) return mean;
@@ -739,8 +786,9 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
       const int64_t nrows = F * D;
       const int64_t grid = std::min<int64_t>(nrows, slots);
       static const int nts = getenv("FMX_CS_NT") ? atoi(getenv("FMX_CS_NT")) : 0;   // A/B: nontemporal stores
+      CsrZc zc{};
       void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
-                       (void*)&stats, (void*)&Y2, (void*)&nts};
+                       (void*)&stats, (void*)&Y2, (void*)&nts, (void*)&zc};
       FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
       return FMX_OK;
     }
@@ -758,6 +806,51 @@ extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int6
   FMX_ARG(op >= FMX_CS_ZSCORE && op <= FMX_CS_MARKET_NEUTRALIZE, "unknown cs op");
   return cs_moment_launch(op, X, Y, F, D, A, ld, present, nullptr, stream);
 }
+
+// The wide Gram's z pass (FMX_CS_GRAM_Z above) over dates [dc0, dc0 + ndc) of X [F][D][ld]:
+// the row stats in numpy's pairwise order (as fmx_cs_moment_stats), Zc [F][ndc][apad] and the
+// validity bits [F][nd_all][nwd] (rows of this chunk).  FMX_ERR_UNSUPPORTED when the row does
+// not fit the register-resident kernel (the caller keeps the stats + tile-kernel z path).
+namespace fmx {
+bool gram_zc_fits(int64_t A) {
+  if (A < 8 || ceil_div(A, (int64_t)32) > CSR_ZC_WORDS) return false;
+  const int slen = pw_len((int)A);
+  if (slen > PW_LDS_MAX) return false;
+  std::vector<int32_t> sh(slen);
+  fmx_debug_pw_schedule((int32_t)A, sh.data(), slen);
+  bool fits = sh[1] > 0 && sh[1] <= CSR_NT / 8;
+  for (int k = 0; fits && k < sh[1]; ++k) fits = sh[5 + sh[1] + k] <= 8 * CSR_EL;
+  return fits;
+}
+
+fmx_status gram_zc_pass(const double* X, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t dc0, int64_t ndc,
+                        double* Zc, int64_t apad, uint32_t* bits, int64_t nd_all, int64_t nwd, void* stream) {
+  if (F == 0 || ndc == 0 || A == 0) return FMX_OK;
+  if (!gram_zc_fits(A) || nwd != ceil_div(A, (int64_t)32) || apad < A) return FMX_ERR_UNSUPPORTED;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  int slen = pw_len((int)A);
+  const void* kr = (const void*)k_cs_moment_rg<FMX_CS_GRAM_Z>;
+  static const int64_t slots = [kr] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kr, CSR_NT, 0) != hipSuccess)
+      return (int64_t)256;
+    return (int64_t)std::max(1, per) * std::max(1, cus);
+  }();
+  const int64_t nrows = F * ndc;
+  FMX_ARG(nrows <= 0x7fffffffll, "too many rows");
+  const int64_t grid = std::min<int64_t>(nrows, slots);
+  CsrZc zc{Zc, bits, ndc, D, dc0, apad, nd_all, (int)nwd};
+  double *Y = nullptr, *stats = nullptr, *Y2 = nullptr;
+  int nts = 0;
+  void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
+                   (void*)&stats, (void*)&Y2, (void*)&nts, (void*)&zc};
+  FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
+  return FMX_OK;
+}
+}  // namespace fmx
 
 extern "C" fmx_status fmx_cs_moment_stats(int32_t op, const double* X, double* Y, int64_t F, int64_t D, int64_t A,
                                           int64_t ld, const uint8_t* present, double* stats, void* stream) {

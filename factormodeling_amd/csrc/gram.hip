@@ -12,6 +12,7 @@
 // The K-slices are reduced in a fixed order by k_gram_reduce (deterministic for any
 // slice -> XCD placement).
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include <cstdlib>
@@ -1262,7 +1263,9 @@ __device__ __forceinline__ void gw_tile(int t, int64_t F, int& bi, int& bj) {
   bj = 2 * bi + t;
 }
 
-template <bool VEC>
+// ZC: X is the z pass's Zc chunk [F][nd][A] (z-scores, invalid -> 0, A a multiple of GW_K
+// with zero pads): staged as loaded, no row stats, no validity bits.
+template <bool VEC, bool ZC = false>
 __global__ void __launch_bounds__(1024)
 k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_t F, int64_t D, int64_t A, int64_t ld,
             int64_t d0, int64_t d1, int64_t dates_per_slice, int64_t phase, int64_t ntile, int64_t nslice, int xcd,
@@ -1349,9 +1352,11 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
 #pragma unroll
       for (int q = 0; q < 2; ++q) rb[q] = (rowB && a0 + bc + q < A32) ? pb[q] : qnan();
     }
-    const double2* z = reinterpret_cast<const double2*>(zst);   // [F][D] (mean, 1/sd or 0)
-    sa = rowA ? z[(int64_t)rA * D + d] : make_double2(0.0, 0.0);
-    sb = rowB ? z[(int64_t)rB * D + d] : make_double2(0.0, 0.0);
+    if constexpr (!ZC) {
+      const double2* z = reinterpret_cast<const double2*>(zst);   // [F][D] (mean, 1/sd or 0)
+      sa = rowA ? z[(int64_t)rA * D + d] : make_double2(0.0, 0.0);
+      sb = rowB ? z[(int64_t)rB * D + d] : make_double2(0.0, 0.0);
+    }
   };
   // validity bits: the diagonal tiles (bj = 2 bi, whose i-rows cover every row once per
   // date) write them while staging -- half-word (16 assets) per row and chunk, in the
@@ -1360,8 +1365,8 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
   auto stage = [&](int buf, int64_t) {
     double* As = gsm + buf * BUF;
     double* Bs = As + GW_I * GW_KP;
-    const bool oka = sa.y > 0.0, okb = sb.y > 0.0;           // 1/sd > 0 <=> sd > 0
-    if (wbits) {                                             // workgroup-uniform
+    const bool oka = !ZC && sa.y > 0.0, okb = !ZC && sb.y > 0.0;   // 1/sd > 0 <=> sd > 0
+    if (!ZC && wbits) {                                      // workgroup-uniform
       // the row's 16 bits in (q, lane & 3) order: any asset order shared by every row
       // gives the same AND / popcount pair counts
       uint32_t hw = 0;
@@ -1375,6 +1380,13 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
       if ((lane & 3) == 0 && rowA) bits16[((int64_t)rA * (d1 - d0) + st_dr) * (2 * nwd) + st_j] = (uint16_t)hw;
     }
     if (++st_j == nch32) { st_j = 0; ++st_dr; }
+    if constexpr (ZC) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = rowA ? ra[q] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) Bs[br * GW_KP + bc + q] = rowB ? rb[q] : 0.0;
+      return;
+    }
 #if GW_DIAG == 4
 #pragma unroll
     for (int q = 0; q < 4; ++q) As[ar * GW_KP + ac + q] = ra[q];
@@ -1453,8 +1465,129 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
       }
 }
 
+// The Zc tile kernel with LDS-DMA staging (global_load_lds_dwordx4): the same 256 x 128 tiles,
+// 16 waves of 64 x 32 sub-tiles and 16-asset chunks as k_gram_f64w<true, true>, but a chunk
+// goes HBM -> LDS with no VGPRs and no staging instructions, three buffers deep: chunk c + 2
+// is in flight while chunk c is multiplied, each wave retires its own DMA of chunk c + 1 with
+// a counted vmcnt and one raw s_barrier per chunk publishes it to every wave.
+// LDS image: 128-B rows (16 doubles), 16-B slot s of row r stored at slot s ^ ((r >> 1) & 7)
+// -- the 16 rows one fragment read touches fall in 16 distinct 16-B positions of a bank row.
+// A DMA wave-instruction fills 8 rows (1 KB); its lane L writes row 8q + (L >> 3), physical
+// slot L & 7, so it loads the logical slot (L & 7) ^ ((row >> 1) & 7) from the row's chunk.
+// Rows past F read row F - 1 (finite z-scores; their products land in rows / columns >= F,
+// never folded).  Zc rows are [nd][A] contiguous: chunk c of a slice is 16 c doubles on.
+constexpr int GZ_BUF = (GW_I + GW_J) * GW_K;                 // doubles per buffer (48 KB)
+constexpr size_t GRAM_Z_LDS = sizeof(double) * 3 * GZ_BUF;     // 144 KB
+__global__ void __launch_bounds__(1024)
+k_gram_zw(const double* __restrict__ Z, int64_t F, int64_t nd, int64_t A, int64_t dps, int64_t phase,
+          int64_t ntile, int64_t nslice, double* __restrict__ part) {
+  extern __shared__ double gsm[];
+  const int64_t total = ntile * nslice, wg = blockIdx.x;
+  const int64_t per = (total + 7) / 8;
+  const int64_t item = (wg % 8) * per + wg / 8;    // XCD-contiguous runs of items, as k_gram_f64w
+  if (item >= total) return;                       // whole workgroup: before any barrier
+  const int64_t tile = item % ntile, slice = item / ntile;
+  int bi, bj;
+  gw_tile((int)tile, F, bi, bj);
+  const int i0 = bi * GW_I, j0 = bj * GW_J;
+  const int64_t ds = slice == 0 ? 0 : slice * dps - phase;
+  const int64_t de = min<int64_t>(nd, (slice + 1) * dps - phase);
+  const int64_t nchunk = (de - ds) * (A / GW_K);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  dbl4 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
+  uint32_t live = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int gi = i0 + wr * 64 + m * 16, gj = j0 + wc * 32 + n * 16;
+      if (gi <= gj + 15 && gi < F && gj < F) live |= 1u << (m * 2 + n);
+    }
+  // this wave's three DMA pieces per chunk: A rows 8 wid + (L >> 3) and 128 + 8 wid + ...,
+  // B rows 8 wid + (L >> 3); source pointers at the slice's first chunk
+  const int lr = lane >> 3;
+  auto src = [&](int lrow, int grow) -> const double* {
+    const int r = min(grow, (int)F - 1);
+    const int sl = (lane & 7) ^ ((lrow >> 1) & 7);
+    return Z + ((int64_t)r * nd + ds) * A + 2 * sl;
+  };
+  const double* pa0 = src(8 * wid + lr, i0 + 8 * wid + lr);
+  const double* pa1 = src(128 + 8 * wid + lr, i0 + 128 + 8 * wid + lr);
+  const double* pb = src(8 * wid + lr, j0 + 8 * wid + lr);
+  auto dma = [&](int64_t c) {
+#if GW_DIAG == 5
+    return;                                          // diagnostics: no DMA (garbage operands)
+#endif
+    double* buf = gsm + (c % 3) * GZ_BUF;
+    typedef __attribute__((address_space(3))) void lds_t;
+    __builtin_amdgcn_global_load_lds((const void*)(pa0 + c * GW_K), (lds_t*)(buf + wid * 8 * GW_K), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(pa1 + c * GW_K), (lds_t*)(buf + (128 + wid * 8) * GW_K), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(pb + c * GW_K), (lds_t*)(buf + (GW_I + wid * 8) * GW_K), 16, 0, 0);
+  };
+  // fragment reads: row r (r & 15 = lane & 15), k = kk + g: logical slot k >> 1, half g & 1
+  const int g = lane >> 4, r16 = lane & 15;
+  if (nchunk > 0) dma(0);
+  if (nchunk > 1) dma(1);
+  if (nchunk > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // waves whose eight 16 x 16 blocks are all live (all but the diagonal / edge tiles') run the
+  // chunk loop without per-MFMA branches; both forms pass the same barriers
+  auto run = [&](auto full) {
+    for (int64_t c = 0; c < nchunk; ++c) {
+      if (c + 2 < nchunk) dma(c + 2);               // buffer (c + 2) % 3 was last read in chunk c - 1
+      const double* As = gsm + (c % 3) * GZ_BUF;
+      const double* Bs = As + GW_I * GW_K;
+#pragma unroll
+      for (int kk = 0; kk < GW_K; kk += 4) {
+        const int k = kk + g;
+        double af[4], bf[2];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int row = wr * 64 + m * 16 + r16;
+          af[m] = As[row * GW_K + (((k >> 1) ^ ((row >> 1) & 7)) << 1) + (k & 1)];
+        }
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int row = wc * 32 + n * 16 + r16;
+          bf[n] = Bs[row * GW_K + (((k >> 1) ^ ((row >> 1) & 7)) << 1) + (k & 1)];
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+            if (decltype(full)::value || ((live >> (m * 2 + n)) & 1u))
+              acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // chunk c + 1 landed (this wave's DMA); chunk c + 2's three may stay in flight
+      if (c + 2 < nchunk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  };
+  if (__builtin_amdgcn_readfirstlane(live) == 0xffu) run(std::true_type{});
+  else run(std::false_type{});
+  double* p = part + (slice * ntile + tile) * (GW_I * GW_J);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;
+        const int col = wc * 32 + n * 16 + (lane & 15);
+        p[row * GW_J + col] = acc[m][n][r];
+      }
+}
+
 // (mean, sd) -> (mean, 1/sd), 0 for sigma in {0, NaN}: the tile kernel's staging multiplies
-__global__ void k_inv_stats(const double* __restrict__ stats, double* __restrict__ zi, int64_t n) {
+__global__ void k_inv_stats(const double* stats, double* zi, int64_t n) {   // in place allowed
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const double m = stats[2 * e], sd = stats[2 * e + 1];
@@ -1664,10 +1797,14 @@ k_gram_fold_w(const double* __restrict__ part, int64_t nslice, int64_t ntile, in
 struct DirectPlan {
   GramPlan g;                                   // g.ntile: k_gram_f64w tiles (256 x 128)
   int64_t nd, nwd, nw;
+  int64_t zc_slices = 0, apad = 0;              // z-pass mode: slices per Zc chunk, padded row
   int64_t bits_bytes() const { return SmallPlan::align256((int64_t)sizeof(uint32_t) * F * nw); }
   int64_t part_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * g.nslice * g.ntile * GW_I * GW_J); }
   int64_t cnt_bytes() const { return (int64_t)sizeof(unsigned long long) * F * F; }
-  int64_t inv_bytes() const { return SmallPlan::align256((int64_t)sizeof(double) * 2 * F * D); }
+  int64_t inv_bytes() const {
+    return zc_slices ? SmallPlan::align256((int64_t)sizeof(double) * F * zc_slices * FMX_GRAM_DATE_BLOCK * apad)
+                     : SmallPlan::align256((int64_t)sizeof(double) * 2 * F * D);
+  }
   int64_t bytes() const { return bits_bytes() + part_bytes() + SmallPlan::align256(cnt_bytes()) + inv_bytes(); }
   int64_t F, D;
 };
@@ -1799,7 +1936,17 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
 // fp64 partial tiles fold into fixed-point limbs (exactsum.hpp).  A date shard whose bounds
 // are multiples of the block holds whole blocks, so every block's partial -- and the integer
 // sum over blocks and ranks -- is the same at 1, 2, 4 or 8 GPUs.
-static DirectPlan direct_exact_plan(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int64_t phase) {
+// z-pass mode (default where the row fits the register-resident moment kernel, A <= 8192;
+// FMX_GRAM_ZC=0 keeps the stats + z-while-staging form): the dates run in chunks of
+// zc_slices date blocks -- a z pass (row moments, Zc, validity bits) then the tile kernel on
+// Zc with no staging arithmetic.  32 blocks of C4's 72 tiles make 9 full rounds of the CUs;
+// the Zc chunk is capped at 32 GB.
+static bool gram_zc_enabled(int64_t A) {
+  static const int on = [] { const char* e = getenv("FMX_GRAM_ZC"); return e ? atoi(e) : 1; }();
+  return on && gram_zc_fits(A);
+}
+static DirectPlan direct_exact_plan(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1, int64_t phase,
+                                    bool zc = false) {
   DirectPlan p;
   p.F = F;
   p.D = D;
@@ -1810,6 +1957,11 @@ static DirectPlan direct_exact_plan(int64_t F, int64_t D, int64_t A, int64_t d0,
   p.nd = d1 - d0;
   p.nwd = ceil_div(A, (int64_t)32);
   p.nw = p.nd * p.nwd;
+  if (zc) {
+    p.apad = ceil_div(A, (int64_t)GW_K) * GW_K;
+    const int64_t per_slice = (int64_t)sizeof(double) * F * FMX_GRAM_DATE_BLOCK * p.apad;
+    p.zc_slices = std::max<int64_t>(1, std::min<int64_t>({(int64_t)32, p.g.nslice, ((int64_t)32 << 30) / per_slice}));
+  }
   return p;
 }
 
@@ -1821,16 +1973,17 @@ static int64_t block_phase(int64_t d_origin, int64_t d0) {
 extern "C" int64_t fmx_gram_direct_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, int64_t d1,
                                                     int64_t d_origin) {
   if (F <= 0 || d1 <= d0) return 0;
-  return direct_exact_plan(F, D, A, d0, d1, block_phase(d_origin, d0)).bytes();
+  return direct_exact_plan(F, D, A, d0, d1, block_phase(d_origin, d0), gram_zc_enabled(A)).bytes();
 }
 
 extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts,
                                             int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1,
                                             int64_t d_origin, int32_t accumulate, void* work, int64_t work_bytes,
                                             void* stream) {
-  FMX_ARG(X && stats && limbs && counts, "null pointer");
+  const bool zc = gram_zc_enabled(A);
+  FMX_ARG(X && limbs && counts, "null pointer");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && d0 >= 0 && d1 <= D && d0 <= d1 && d_origin >= 0, "bad dims");
-  FMX_ARG(F <= 65535 && d1 - d0 <= 0x7fffffff, "too many factors / dates");
+  FMX_ARG(F <= 65535 && d1 - d0 <= 0x7fffffff && A <= 0x7fffffff, "too many factors / dates / assets");
   hipStream_t st = as_stream(stream);
   if (!accumulate && F > 0) {
     FMX_HIP(hipMemsetAsync(limbs, 0, sizeof(int64_t) * FMX_GRAM_EXACT_SLOTS * F * F, st));
@@ -1838,14 +1991,55 @@ extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats
   }
   if (F == 0 || d1 == d0 || A == 0) return FMX_OK;
   const int64_t phase = block_phase(d_origin, d0);
-  const DirectPlan pl = direct_exact_plan(F, D, A, d0, d1, phase);
+  const DirectPlan pl = direct_exact_plan(F, D, A, d0, d1, phase, zc);
   if (fmx_status e = check_work(work, work_bytes, pl.bytes(), "fmx_gram_direct_exact_work_bytes")) return e;
   char* w = static_cast<char*>(work);
   uint32_t* bits = reinterpret_cast<uint32_t*>(w);
   double* part = reinterpret_cast<double*>(w + pl.bits_bytes());
   unsigned long long* ncnt = reinterpret_cast<unsigned long long*>(w + pl.bits_bytes() + pl.part_bytes());
   double* zinv = reinterpret_cast<double*>(w + pl.bits_bytes() + pl.part_bytes() + SmallPlan::align256(pl.cnt_bytes()));
+  if (zc) {
+    // chunks of zc_slices absolute date blocks: z pass over the chunk's dates into Zc (the
+    // zinv region), then the tile kernel on Zc; slice s of the whole range covers dates
+    // [d0 + 16 s - phase, d0 + 16 (s + 1) - phase) clipped to [d0, d1)
+    double* Zc = zinv;
+    const int64_t ntile = pl.g.ntile, nsl = pl.g.nslice, dps = FMX_GRAM_DATE_BLOCK, apad = pl.apad, nwd = pl.nwd;
+    static const int glds = [] { const char* e = getenv("FMX_GRAM_GLDS"); return e ? atoi(e) : 1; }();
+    const void* k = glds ? (const void*)k_gram_zw : (const void*)k_gram_f64w<true, true>;
+    const size_t klds = glds ? GRAM_Z_LDS : GRAM_W_LDS;
+    FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)klds));
+    for (int64_t s0 = 0; s0 < nsl; s0 += pl.zc_slices) {
+      const int64_t s1 = std::min(nsl, s0 + pl.zc_slices);
+      const int64_t dc0 = s0 == 0 ? d0 : d0 + s0 * dps - phase, dc1 = std::min(d1, d0 + s1 * dps - phase);
+      const int64_t ndc = dc1 - dc0;
+      if (fmx_status e = gram_zc_pass(X, F, D, A, ld, dc0, ndc, Zc, apad, bits + (dc0 - d0) * nwd, d1 - d0, nwd, st))
+        return e;
+      const double* zx = Zc;
+      const double* znull = nullptr;
+      int64_t Dz = ndc, Az = apad, lz = apad, z0 = 0, z1 = ndc, ph = s0 == 0 ? phase : 0, nsc = s1 - s0;
+      int xcd_arg = 1, wopt_arg = 1;
+      double* pc = part + s0 * ntile * (GW_I * GW_J);
+      uint16_t* nob = nullptr;
+      const int64_t nwg = 8 * ((ntile * nsc + 7) / 8);
+      void* args[] = {(void*)&zx, (void*)&znull, (void*)&F, (void*)&Dz, (void*)&Az, (void*)&lz, (void*)&z0, (void*)&z1,
+                      (void*)&dps, (void*)&ph, (void*)&ntile, (void*)&nsc, (void*)&xcd_arg, (void*)&wopt_arg,
+                      (void*)&pc, (void*)&nob, (void*)&nwd};
+      void* zargs[] = {(void*)&zx, (void*)&F, (void*)&Dz, (void*)&Az, (void*)&dps, (void*)&ph, (void*)&ntile, (void*)&nsc,
+                       (void*)&pc};
+      FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nwg), dim3(1024), glds ? zargs : args, klds, st));
+    }
+    FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
+    if (fmx_status e = launch_pair_counts(bits, F, pl.nw, ncnt, st)) return e;
+    k_gram_fold_w<<<dim3((unsigned)ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, nsl, ntile, F, ncnt, limbs, counts,
+                                                                            accumulate ? 1 : 0);
+    FMX_LAUNCH_CHECK("k_gram_fold_w");
+    return FMX_OK;
+  }
   if (ceil_div(A, (int64_t)GW_K) % 2 == 1) FMX_HIP(hipMemsetAsync(bits, 0, pl.bits_bytes(), st));
+  if (!stats) {                                   // no caller stats: the row moments in place
+    if (fmx_status e = fmx_cs_moment_stats(FMX_CS_STATS, X, nullptr, F, D, A, ld, nullptr, zinv, stream)) return e;
+    stats = zinv;
+  }
   k_inv_stats<<<(unsigned)ceil_div(F * D, (int64_t)256), 256, 0, st>>>(stats, zinv, F * D);
   FMX_LAUNCH_CHECK("k_inv_stats");
   const double* zst = zinv;

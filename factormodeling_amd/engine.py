@@ -7,6 +7,7 @@ multi-GPU driver are built on.
 """
 from __future__ import annotations
 
+import os
 import ctypes
 
 import numpy as np
@@ -613,7 +614,7 @@ def gram_direct_exact(X, d0=0, d1=None, d_origin=0, stats=None, limbs=None, coun
     F, D, A = X.shape
     d1 = D if d1 is None else d1
     if stats is None:
-        _, stats = cs_moment_stats("stats", X)
+        pass            # the kernel's z pass (or, past its row size, its own stats pass) computes the moments
     elif tuple(stats.shape) != (F, D, 2) or stats.dtype != F64 or not stats.is_contiguous():
         raise _lib.FmxError("stats must be a contiguous float64 [F][D][2] device tensor")
     if limbs is None:
