@@ -1476,11 +1476,23 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
 // slot L & 7, so it loads the logical slot (L & 7) ^ ((row >> 1) & 7) from the row's chunk.
 // Rows past F read row F - 1 (finite z-scores; their products land in rows / columns >= F,
 // never folded).  Zc rows are [nd][A] contiguous: chunk c of a slice is 16 c doubles on.
+#ifndef GZ_PF
+#define GZ_PF 1        // fragment reads one k-step ahead of the MFMAs (0: A/B arm, 0.7 ms slower per 252 C4 dates)
+#endif
+#ifndef GZ_PRIO
+#define GZ_PRIO 0      // A/B: raised wave priority around each MFMA burst
+#endif
 constexpr int GZ_BUF = (GW_I + GW_J) * GW_K;                 // doubles per buffer (48 KB)
 constexpr size_t GRAM_Z_LDS = sizeof(double) * 3 * GZ_BUF;     // 144 KB
-__global__ void __launch_bounds__(1024)
+// NW = 16: waves as 4 x 4 of 64 x 32 sub-tiles (4 x 2 MFMA blocks, 4 waves per SIMD);
+// NW = 8: 4 x 2 of 64 x 64 (4 x 4 blocks: twice the MFMAs per fragment read, 2 waves per SIMD).
+template <int NW>
+__global__ void __launch_bounds__(NW * 64)
 k_gram_zw(const double* __restrict__ Z, int64_t F, int64_t nd, int64_t A, int64_t dps, int64_t phase,
           int64_t ntile, int64_t nslice, double* __restrict__ part) {
+  constexpr int WC = NW / 4, NBN = GW_J / WC / 16;           // wave columns, 16-blocks per wave row
+  constexpr int PA = (GW_I / 8) / NW, PB = (GW_J / 8) / NW;  // DMA pieces per wave and chunk
+  constexpr int NP = PA + PB;
   extern __shared__ double gsm[];
   const int64_t total = ntile * nslice, wg = blockIdx.x;
   const int64_t per = (total + 7) / 8;
@@ -1494,94 +1506,139 @@ k_gram_zw(const double* __restrict__ Z, int64_t F, int64_t nd, int64_t A, int64_
   const int64_t de = min<int64_t>(nd, (slice + 1) * dps - phase);
   const int64_t nchunk = (de - ds) * (A / GW_K);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  dbl4 acc[4][2];
+  const int wr = wid / WC, wc = wid % WC;
+  dbl4 acc[4][NBN];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int n = 0; n < NBN; ++n) acc[m][n] = dbl4{0.0, 0.0, 0.0, 0.0};
   uint32_t live = 0;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int gi = i0 + wr * 64 + m * 16, gj = j0 + wc * 32 + n * 16;
-      if (gi <= gj + 15 && gi < F && gj < F) live |= 1u << (m * 2 + n);
+    for (int n = 0; n < NBN; ++n) {
+      const int gi = i0 + wr * 64 + m * 16, gj = j0 + wc * (16 * NBN) + n * 16;
+      if (gi <= gj + 15 && gi < F && gj < F) live |= 1u << (m * NBN + n);
     }
-  // this wave's three DMA pieces per chunk: A rows 8 wid + (L >> 3) and 128 + 8 wid + ...,
-  // B rows 8 wid + (L >> 3); source pointers at the slice's first chunk
+  constexpr uint32_t ALL = (1u << (4 * NBN)) - 1u;
+  // this wave's DMA pieces per chunk: A row groups wid + NW q (rows 8 group + (L >> 3)), B
+  // row groups wid + NW q; source pointers at the slice's first chunk
   const int lr = lane >> 3;
   auto src = [&](int lrow, int grow) -> const double* {
     const int r = min(grow, (int)F - 1);
     const int sl = (lane & 7) ^ ((lrow >> 1) & 7);
     return Z + ((int64_t)r * nd + ds) * A + 2 * sl;
   };
-  const double* pa0 = src(8 * wid + lr, i0 + 8 * wid + lr);
-  const double* pa1 = src(128 + 8 * wid + lr, i0 + 128 + 8 * wid + lr);
-  const double* pb = src(8 * wid + lr, j0 + 8 * wid + lr);
+  const double* pp[NP];
+#pragma unroll
+  for (int q = 0; q < PA; ++q) pp[q] = src(8 * (wid + NW * q) + lr, i0 + 8 * (wid + NW * q) + lr);
+#pragma unroll
+  for (int q = 0; q < PB; ++q) pp[PA + q] = src(8 * (wid + NW * q) + lr, j0 + 8 * (wid + NW * q) + lr);
   auto dma = [&](int64_t c) {
-#if GW_DIAG == 5
+#if GW_DIAG == 5 || GW_DIAG == 7
     return;                                          // diagnostics: no DMA (garbage operands)
 #endif
     double* buf = gsm + (c % 3) * GZ_BUF;
     typedef __attribute__((address_space(3))) void lds_t;
-    __builtin_amdgcn_global_load_lds((const void*)(pa0 + c * GW_K), (lds_t*)(buf + wid * 8 * GW_K), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(pa1 + c * GW_K), (lds_t*)(buf + (128 + wid * 8) * GW_K), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(pb + c * GW_K), (lds_t*)(buf + (GW_I + wid * 8) * GW_K), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int row = q < PA ? 8 * (wid + NW * q) : GW_I + 8 * (wid + NW * (q - PA));
+      __builtin_amdgcn_global_load_lds((const void*)(pp[q] + c * GW_K), (lds_t*)(buf + row * GW_K), 16, 0, 0);
+    }
+  };
+  auto wait_dma = [&](bool keep) {                 // keep: the newest chunk's NP pieces stay in flight
+    if (keep) {
+      if constexpr (NP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
   // fragment reads: row r (r & 15 = lane & 15), k = kk + g: logical slot k >> 1, half g & 1
   const int g = lane >> 4, r16 = lane & 15;
   if (nchunk > 0) dma(0);
   if (nchunk > 1) dma(1);
-  if (nchunk > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_dma(nchunk > 1);
   __builtin_amdgcn_s_barrier();
-  // waves whose eight 16 x 16 blocks are all live (all but the diagonal / edge tiles') run the
+  // waves whose 16 x 16 blocks are all live (all but the diagonal / edge tiles') run the
   // chunk loop without per-MFMA branches; both forms pass the same barriers
   auto run = [&](auto full) {
     for (int64_t c = 0; c < nchunk; ++c) {
       if (c + 2 < nchunk) dma(c + 2);               // buffer (c + 2) % 3 was last read in chunk c - 1
       const double* As = gsm + (c % 3) * GZ_BUF;
       const double* Bs = As + GW_I * GW_K;
-#pragma unroll
-      for (int kk = 0; kk < GW_K; kk += 4) {
+      auto frag = [&](int kk, double* af, double* bf) {
         const int k = kk + g;
-        double af[4], bf[2];
+#if GW_DIAG == 6
+#pragma unroll
+        for (int m = 0; m < 4; ++m) af[m] = (double)(k + m);  // diagnostics: no LDS reads
+#pragma unroll
+        for (int n = 0; n < NBN; ++n) bf[n] = (double)(k - n);
+        asm volatile("" : "+v"(af[0]), "+v"(bf[0]));
+        return;
+#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int row = wr * 64 + m * 16 + r16;
           af[m] = As[row * GW_K + (((k >> 1) ^ ((row >> 1) & 7)) << 1) + (k & 1)];
         }
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int row = wc * 32 + n * 16 + r16;
+        for (int n = 0; n < NBN; ++n) {
+          const int row = wc * (16 * NBN) + n * 16 + r16;
           bf[n] = Bs[row * GW_K + (((k >> 1) ^ ((row >> 1) & 7)) << 1) + (k & 1)];
         }
+      };
+      auto mm = [&](const double* af, const double* bf) {
+#if GZ_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
-            if (decltype(full)::value || ((live >> (m * 2 + n)) & 1u))
+          for (int n = 0; n < NBN; ++n)
+            if (decltype(full)::value || ((live >> (m * NBN + n)) & 1u))
               acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[n], acc[m][n], 0, 0, 0);
+#if GZ_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      };
+#if GZ_PF
+      // next k-step's fragments are read before this step's MFMAs (two sets live)
+      double af0[4], bf0[NBN], af1[4], bf1[NBN];
+      frag(0, af0, bf0);
+      frag(4, af1, bf1);
+      mm(af0, bf0);
+      frag(8, af0, bf0);
+      mm(af1, bf1);
+      frag(12, af1, bf1);
+      mm(af0, bf0);
+      mm(af1, bf1);
+#else
+#pragma unroll
+      for (int kk = 0; kk < GW_K; kk += 4) {
+        double af[4], bf[NBN];
+        frag(kk, af, bf);
+        mm(af, bf);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // chunk c + 1 landed (this wave's DMA); chunk c + 2's three may stay in flight
-      if (c + 2 < nchunk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      wait_dma(c + 2 < nchunk);                     // chunk c + 1 landed (this wave's DMA)
+#if GW_DIAG != 7
       __builtin_amdgcn_s_barrier();
+#endif
     }
   };
-  if (__builtin_amdgcn_readfirstlane(live) == 0xffu) run(std::true_type{});
+  if (__builtin_amdgcn_readfirstlane(live) == ALL) run(std::true_type{});
   else run(std::false_type{});
   double* p = part + (slice * ntile + tile) * (GW_I * GW_J);
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < NBN; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;
-        const int col = wc * 32 + n * 16 + (lane & 15);
+        const int col = wc * (16 * NBN) + n * 16 + (lane & 15);
         p[row * GW_J + col] = acc[m][n][r];
       }
 }
@@ -2004,8 +2061,11 @@ extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats
     // [d0 + 16 s - phase, d0 + 16 (s + 1) - phase) clipped to [d0, d1)
     double* Zc = zinv;
     const int64_t ntile = pl.g.ntile, nsl = pl.g.nslice, dps = FMX_GRAM_DATE_BLOCK, apad = pl.apad, nwd = pl.nwd;
-    static const int glds = [] { const char* e = getenv("FMX_GRAM_GLDS"); return e ? atoi(e) : 1; }();
-    const void* k = glds ? (const void*)k_gram_zw : (const void*)k_gram_f64w<true, true>;
+    // FMX_GRAM_GLDS: 0 register-staged k_gram_f64w<true, true>, 8 / 16 (default) waves of k_gram_zw
+    static const int glds = [] { const char* e = getenv("FMX_GRAM_GLDS"); return e ? atoi(e) : 16; }();
+    const void* k = glds == 8 ? (const void*)k_gram_zw<8> : glds ? (const void*)k_gram_zw<16>
+                                                                 : (const void*)k_gram_f64w<true, true>;
+    const int nthr = glds == 8 ? 512 : 1024;
     const size_t klds = glds ? GRAM_Z_LDS : GRAM_W_LDS;
     FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)klds));
     for (int64_t s0 = 0; s0 < nsl; s0 += pl.zc_slices) {
@@ -2026,7 +2086,7 @@ extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats
                       (void*)&pc, (void*)&nob, (void*)&nwd};
       void* zargs[] = {(void*)&zx, (void*)&F, (void*)&Dz, (void*)&Az, (void*)&dps, (void*)&ph, (void*)&ntile, (void*)&nsc,
                        (void*)&pc};
-      FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nwg), dim3(1024), glds ? zargs : args, klds, st));
+      FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nwg), dim3(nthr), glds ? zargs : args, klds, st));
     }
     FMX_HIP(hipMemsetAsync(ncnt, 0, pl.cnt_bytes(), st));
     if (fmx_status e = launch_pair_counts(bits, F, pl.nw, ncnt, st)) return e;
