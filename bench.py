@@ -75,7 +75,7 @@ def bytes_per_unit(stage, F, ranked=False):
 # stage -> kernel-name prefix in the rocprofv3 PMC summaries (profiles/traffic_c*.json)
 STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic_daily_fr<"),
                 "ts_set": "fmx::k_ts_set<", "rank2": ("fmx::k_cs_rank2_pf<", "fmx::k_cs_rank_fa<1024, 10, false, false", "fmx::k_cs_rank_fa<"),
-                "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:corr_vol": "fmx::k_ts_corr_feat<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
+                "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:corr_vol": "fmx::k_ts_corr_feat<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_zw<", "fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
                 "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
                 "cs_rank_winsor_zn": "fmx::k_cs_rank_fa<512, 10, false, true, false, true>",
