@@ -346,7 +346,12 @@ int64_t fmx_gram_exact_work_bytes(int64_t F, int64_t D, int64_t A, int64_t d0, i
  * partial tiles fold into the same fixed-point limbs as fmx_gram_exact.  A date shard whose
  * bounds are multiples of FMX_GRAM_DATE_BLOCK holds whole blocks, so an int64 all-reduce of
  * limbs / counts + fmx_gram_exact_finalize gives the same G, N bits at every GPU count.
- * accumulate = 0 zeroes limbs and counts first.  work: fmx_gram_direct_exact_work_bytes. */
+ * accumulate = 0 zeroes limbs and counts first.  work: fmx_gram_direct_exact_work_bytes.
+ * Rows of 8..8192 assets (the default): a z pass computes the row moments itself, writes
+ * zero-filled z-scores for chunks of 32 date blocks into the workspace and an LDS-DMA tile
+ * kernel multiplies them, so stats is ignored and may be NULL.  Other rows (or
+ * FMX_GRAM_ZC=0) z-score while staging from stats = fmx_cs_moment_stats (mean, std) [F][D][2];
+ * NULL there computes them into the workspace first. */
 #define FMX_GRAM_DATE_BLOCK 16
 fmx_status fmx_gram_direct_exact(const double* X, const double* stats, int64_t* limbs, int64_t* counts, int64_t F,
                                  int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int64_t d_origin,
