@@ -810,6 +810,12 @@ static SmallPlan small_plan(int64_t F, int64_t A, int64_t d0, int64_t d1) {
   return p;
 }
 
+}  // namespace fmx
+// pair counts of k_gram_db's chunk-major validity bits (defined with k_gram_cnt_i8 below)
+static fmx_status launch_pair_counts_cm(const uint32_t* mbits, int64_t F, int64_t nw, int FP,
+                                        unsigned long long* ncnt, hipStream_t st);
+namespace fmx {
+
 template <int NB>
 static fmx_status gram_small_launch(const double* X, const double* stats, double* G, double* N, int64_t F,
                                     int64_t D, int64_t A, int64_t ld, int64_t d0, int64_t d1, int accumulate,
@@ -851,13 +857,7 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
                                                            nullptr);
     FMX_LAUNCH_CHECK("k_gram_small<N>");
   } else if (nw > 0) {
-    const int T = (int)ceil_div(F, (int64_t)32);
-    const int ntile = T * (T + 1) / 2;
-    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PC_W), 2048 / ntile + 1));
-    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PC_W) * PC_W;
-    const unsigned nky = (unsigned)ceil_div(nw, wps);
-    k_gram_popc<<<dim3((unsigned)ntile, nky), 256, 0, st>>>(mbits, F, nw, wps, FP, ncnt);
-    FMX_LAUNCH_CHECK("k_gram_popc");
+    if (fmx_status e = launch_pair_counts_cm(mbits, F, nw, FP, ncnt, st)) return e;
   }
   k_gram_small_reduce<<<(unsigned)ceil_div((int64_t)FP * FP, 256), 256, 0, st>>>(
       part, mask_mfma ? part + st_elems : nullptr, nslice, FP, F, G, N, accumulate, mask_mfma ? nullptr : ncnt);
@@ -920,14 +920,8 @@ static fmx_status gram_exact_launch(const double* X, const double* stats, int64_
                                                                    nslice, part, mbits, gopt, (int)pl.S);
   FMX_LAUNCH_CHECK("k_gram_db<units>");
   {
-    const int T = (int)ceil_div(F, (int64_t)32);
-    const int ntile = T * (T + 1) / 2;
     const int64_t nw = pl.nw;
-    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PC_W), 2048 / ntile + 1));
-    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PC_W) * PC_W;
-    const unsigned nky = (unsigned)ceil_div(nw, wps);
-    k_gram_popc<<<dim3((unsigned)ntile, nky), 256, 0, st>>>(mbits, F, nw, wps, FP, ncnt);
-    FMX_LAUNCH_CHECK("k_gram_popc");
+    if (fmx_status e = launch_pair_counts_cm(mbits, F, nw, FP, ncnt, st)) return e;
   }
   const int64_t ngroups = std::max<int64_t>(1, std::min<int64_t>(pl.nunits, 2048 / pl.ntri));
   const int64_t upg = ceil_div(pl.nunits, ngroups);
@@ -1742,10 +1736,13 @@ __device__ __forceinline__ gc_v4i gc_expand(uint32_t t) {
   d[3] = (int)((t >> 3) & M);
   return d;
 }
-template <bool VEC>
+// CM: chunk-major bits [nw][F] (k_gram_db's mbits) instead of factor-major [F][nw]; ldn: the
+// row stride of ncnt; btri: every pair of a 16 x 16 block on or above the block diagonal
+// (k_gram_small_reduce / k_gram_fold's map) instead of the pairs i <= j.
+template <bool VEC, bool CM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_gram_cnt_i8(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t wps,
-              unsigned long long* __restrict__ ncnt) {
+              unsigned long long* __restrict__ ncnt, int64_t ldn = 0, int btri = 0) {
   __shared__ uint32_t Ls[2 * GC_T * GC_LP];                   // rows 0..127: I tile, 128..255: J
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int tt = blockIdx.x, ti = 0;
@@ -1764,24 +1761,38 @@ k_gram_cnt_i8(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t 
   const int lr = tid >> 2, lw = (tid & 3) * 4;
   for (int64_t wc0 = w0; wc0 < w1; wc0 += GC_KW) {
     uint32_t v[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = lr + 64 * i;
-      const int64_t fr = row < GC_T ? I0 + row : J0 + row - GC_T;
-      const uint32_t* p = bits + fr * nw + wc0 + lw;
+    if constexpr (CM) {
+      // thread t: row t of the 256 (I then J), the chunk's 16 words (a word's rows are contiguous)
+      const int64_t fr = tid < GC_T ? I0 + tid : J0 + tid - GC_T;
       const bool ok = fr < F;
-      if (VEC && ok && wc0 + lw + 4 <= w1) {
-        const uint4 u = *reinterpret_cast<const uint4*>(p);
-        v[i][0] = u.x; v[i][1] = u.y; v[i][2] = u.z; v[i][3] = u.w;
-      } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[i][q] = (ok && wc0 + lw + q < w1) ? p[q] : 0u;
+      for (int q = 0; q < 16; ++q) v[q >> 2][q & 3] = (ok && wc0 + q < w1) ? bits[(wc0 + q) * F + fr] : 0u;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lr + 64 * i;
+        const int64_t fr = row < GC_T ? I0 + row : J0 + row - GC_T;
+        const uint32_t* p = bits + fr * nw + wc0 + lw;
+        const bool ok = fr < F;
+        if (VEC && ok && wc0 + lw + 4 <= w1) {
+          const uint4 u = *reinterpret_cast<const uint4*>(p);
+          v[i][0] = u.x; v[i][1] = u.y; v[i][2] = u.z; v[i][3] = u.w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[i][q] = (ok && wc0 + lw + q < w1) ? p[q] : 0u;
+        }
       }
     }
     __syncthreads();                                          // the previous chunk's reads are done
+    if constexpr (CM) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<uint4*>(&Ls[(lr + 64 * i) * GC_LP + lw]) = make_uint4(v[i][0], v[i][1], v[i][2], v[i][3]);
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(&Ls[tid * GC_LP + 4 * i]) = make_uint4(v[i][0], v[i][1], v[i][2], v[i][3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(&Ls[(lr + 64 * i) * GC_LP + lw]) = make_uint4(v[i][0], v[i][1], v[i][2], v[i][3]);
+    }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < GC_KW / 2; ++s) {
@@ -1805,7 +1816,8 @@ k_gram_cnt_i8(const uint32_t* __restrict__ bits, int64_t F, int64_t nw, int64_t 
       for (int q = 0; q < 4; ++q) {
         const int gi = I0 + wr * 64 + m * 16 + 4 * g + q, gj = J0 + wc * 64 + n * 16 + r;
         const int c = acc[m][n][q];
-        if (gi < F && gj < F && gi <= gj && c) atomicAdd(&ncnt[(int64_t)gi * F + gj], (unsigned long long)c);
+        const bool up = btri ? (gi >> 4) <= (gj >> 4) : gi <= gj;
+        if (gi < F && gj < F && up && c) atomicAdd(&ncnt[(int64_t)gi * (ldn ? ldn : F) + gj], (unsigned long long)c);
       }
 }
 
@@ -1931,6 +1943,34 @@ static fmx_status launch_pair_counts(const uint32_t* bits, int64_t F, int64_t nw
   if (nw % 4 == 0) k_gram_cnt_i8<true><<<grid, 256, 0, st>>>(bits, F, nw, wps, ncnt);
   else k_gram_cnt_i8<false><<<grid, 256, 0, st>>>(bits, F, nw, wps, ncnt);
   FMX_LAUNCH_CHECK("k_gram_cnt_i8");
+  return FMX_OK;
+}
+
+// k_gram_db's counts: chunk-major bits [nw][F] into ncnt [FP][FP], every pair of the 16 x 16
+// blocks on or above the block diagonal (FMX_GRAM_CNT=0: the AND / popcount kernel)
+static fmx_status launch_pair_counts_cm(const uint32_t* mbits, int64_t F, int64_t nw, int FP,
+                                        unsigned long long* ncnt, hipStream_t st) {
+  static const int mode = [] { const char* e = getenv("FMX_GRAM_CNT"); return e ? atoi(e) : 1; }();
+  if (mode == 0) {
+    const int T = (int)ceil_div(F, (int64_t)32);
+    const int ntile = T * (T + 1) / 2;
+    const int64_t nks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(nw, (int64_t)4 * PC_W), 2048 / ntile + 1));
+    const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)PC_W) * PC_W;
+    const unsigned nky = (unsigned)ceil_div(nw, wps);
+    k_gram_popc<<<dim3((unsigned)ntile, nky), 256, 0, st>>>(mbits, F, nw, wps, FP, ncnt);
+    FMX_LAUNCH_CHECK("k_gram_popc");
+    return FMX_OK;
+  }
+  const int T = (int)ceil_div(F, (int64_t)GC_T);
+  const int64_t ntp = (int64_t)T * (T + 1) / 2;
+  const int64_t nchunk = ceil_div(nw, (int64_t)GC_KW);
+  // word slices: ~4 workgroups per CU, whole 16-word chunks, <= 2^25 words per slice
+  int64_t nks = std::max<int64_t>(1, std::min<int64_t>(nchunk, 1024 / ntp));
+  nks = std::max<int64_t>(nks, ceil_div(nw, (int64_t)1 << 25));
+  const int64_t wps = ceil_div(ceil_div(nw, nks), (int64_t)GC_KW) * GC_KW;
+  k_gram_cnt_i8<false, true><<<dim3((unsigned)ntp, (unsigned)ceil_div(nw, wps)), 256, 0, st>>>(mbits, F, nw, wps, ncnt,
+                                                                                               (int64_t)FP, 1);
+  FMX_LAUNCH_CHECK("k_gram_cnt_i8<cm>");
   return FMX_OK;
 }
 
