@@ -1473,6 +1473,9 @@ k_gram_f64w(const double* __restrict__ X, const double* __restrict__ zst, int64_
 #ifndef GZ_PF
 #define GZ_PF 1        // fragment reads one k-step ahead of the MFMAs (0: A/B arm, 0.7 ms slower per 252 C4 dates)
 #endif
+#ifndef GZ_SGB
+#define GZ_SGB 0       // A/B: the read / MFMA order of the prefetching k-loop pinned by sched_group_barrier
+#endif
 #ifndef GZ_PRIO
 #define GZ_PRIO 0      // A/B: raised wave priority around each MFMA burst
 #endif
@@ -1607,6 +1610,19 @@ k_gram_zw(const double* __restrict__ Z, int64_t F, int64_t nd, int64_t A, int64_
       frag(12, af1, bf1);
       mm(af0, bf0);
       mm(af1, bf1);
+#if GZ_SGB
+      if constexpr (decltype(full)::value) {
+        // pin the order: reads of steps 0, 1 | MFMAs of 0 | reads of 2 | MFMAs of 1 | reads of
+        // 3 | MFMAs of 2, 3 -- so each step's wait leaves the next step's reads in flight
+        constexpr int RD = (4 + NBN) / 2, MF = 4 * NBN;     // ds_read2 per step, MFMAs per step
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * RD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * MF, 0);
+      }
+#endif
 #else
 #pragma unroll
       for (int kk = 0; kk < GW_K; kk += 4) {
