@@ -64,6 +64,7 @@ SIGNATURES = {
     "fmx_gram_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i32],
     "fmx_gram_direct": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     "fmx_gram_direct_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64],
+    "fmx_greedy_prune": [c_vp, c_i64, c_i64, c_vp, c_i64, c_dbl, c_i64, c_vp, c_vp, c_vp],
     "fmx_gram_direct_exact": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp,
                               c_i64, c_vp],
     "fmx_gram_direct_exact_work_bytes": [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64],

@@ -984,6 +984,37 @@ k_window_prune(const double* __restrict__ partG, const double* __restrict__ part
   for (int i = lane; i < nk; i += 64) w[kept[i]] = 1.0 / (double)nk;
 }
 
+// The step's greedy prune over one correlation matrix (pipeline.run_step; the host walk of
+// engine.greedy_prune restated): walk `order`; f is kept iff M(f) = max over the kept k of
+// |C[f, k]| is NaN (a NaN propagates, as np.maximum does) or < rho; stop at top_x kept.
+// One workgroup: M lives in LDS for every factor and absorbs row k of C (= column k: C is
+// symmetric bit for bit) when k is kept, so each candidate costs one LDS read and a barrier,
+// each kept one a coalesced row read.
+constexpr int GP_NT = 1024;
+__device__ __forceinline__ double gp_max(double a, double b) { return (a != a || b != b) ? qnan() : (a > b ? a : b); }
+__global__ void __launch_bounds__(GP_NT)
+k_greedy_prune(const double* __restrict__ C, int64_t F, int64_t ldc, const int64_t* __restrict__ order,
+               int64_t n_order, double rho, int64_t top_x, int32_t* __restrict__ kept, int32_t* __restrict__ n_kept) {
+  extern __shared__ double mx[];                 // [F]
+  const int tid = threadIdx.x;
+  for (int64_t f = tid; f < F; f += GP_NT) mx[f] = -__builtin_inf();
+  __syncthreads();
+  int64_t nk = 0;
+  for (int64_t pos = 0; pos < n_order && nk < top_x; ++pos) {
+    const int64_t c = order[pos];                // block-uniform
+    if (c < 0 || c >= F) continue;
+    const double m = mx[c];
+    if (m == m && m >= rho) continue;            // every thread reads the same value
+    if (tid == 0) kept[nk] = (int32_t)c;
+    ++nk;
+    __syncthreads();                             // all threads have read mx[c]
+    const double* row = C + c * ldc;
+    for (int64_t f = tid; f < F; f += GP_NT) mx[f] = gp_max(mx[f], fabs(row[f]));
+    __syncthreads();
+  }
+  if (tid == 0) *n_kept = (int32_t)nk;
+}
+
 // Workspace of fmx_corr_prune_windows: per-date G and N partials over the dates the
 // windows touch, then the window starts.
 static void prune_dates(int64_t D, int64_t J, int W, const int32_t* s0_host, int64_t& d_lo, int64_t& nd) {
@@ -2174,6 +2205,20 @@ extern "C" fmx_status fmx_gram_direct_exact(const double* X, const double* stats
   k_gram_fold_w<<<dim3((unsigned)ntile, GW_I * GW_J / 256), 256, 0, st>>>(part, nslice, ntile, F, ncnt, limbs, counts,
                                                                           accumulate ? 1 : 0);
   FMX_LAUNCH_CHECK("k_gram_fold_w");
+  return FMX_OK;
+}
+
+extern "C" fmx_status fmx_greedy_prune(const double* C, int64_t F, int64_t ldc, const int64_t* order, int64_t n_order,
+                                       double rho, int64_t top_x, int32_t* kept, int32_t* n_kept, void* stream) {
+  FMX_ARG(C && order && kept && n_kept, "null pointer");
+  FMX_ARG(F >= 0 && ldc >= F && n_order >= 0 && top_x >= 0, "bad dims");
+  FMX_ARG((int64_t)sizeof(double) * F <= 160 * 1024, "too many factors for the LDS walk (F <= 20480)");
+  hipStream_t st = as_stream(stream);
+  const size_t lds = sizeof(double) * std::max<int64_t>(F, 1);
+  if (lds > 64 * 1024)
+    FMX_HIP(hipFuncSetAttribute((const void*)k_greedy_prune, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  k_greedy_prune<<<1, GP_NT, lds, st>>>(C, F, ldc, order, n_order, rho, top_x, kept, n_kept);
+  FMX_LAUNCH_CHECK("k_greedy_prune");
   return FMX_OK;
 }
 

@@ -675,8 +675,30 @@ def corr_prune_windows(X, stats, metrics, order, window: int, s0, use_rank_icir=
     return w
 
 
+def _greedy_prune_device(C, order, rho, top_x):
+    if C.dim() != 2 or C.shape[0] != C.shape[1] or C.dtype != F64:
+        raise _lib.FmxError("greedy_prune: C must be a square float64 matrix")
+    C = C.contiguous()
+    F = C.shape[0]
+    if isinstance(order, torch.Tensor):
+        ordt = order.to(device=C.device, dtype=torch.int64).contiguous()
+    else:
+        ordt = torch.as_tensor(np.asarray(order, dtype=np.int64), device=C.device)
+    # the host walk returns once len(kept) >= top_x after an append: top_x <= 0 keeps one
+    lim = F if top_x is None else max(int(top_x), 1)
+    kept = torch.empty(max(min(lim, F), 1), dtype=torch.int32, device=C.device)
+    nk = torch.zeros(1, dtype=torch.int32, device=C.device)
+    call("fmx_greedy_prune", ptr(C), F, F, ptr(ordt), int(ordt.numel()), float(rho), lim, ptr(kept), ptr(nk),
+         stream_ptr())
+    n = int(nk.item())
+    return [int(v) for v in kept[:n].cpu().tolist()]
+
+
 def greedy_prune(C, order, rho=0.7, top_x=None):
-    """Walk ``order``; keep f iff max |C[f, kept]| < rho (host, O(F * kept))."""
+    """Walk ``order``; keep f iff max |C[f, kept]| < rho (NaN: kept).  A device C runs the
+    walk on the GPU (fmx_greedy_prune: no F x F copy to the host); a host C the numpy walk."""
+    if isinstance(C, torch.Tensor) and C.is_cuda:
+        return _greedy_prune_device(C, order, rho, top_x)
     Cn = C.detach().cpu().numpy() if isinstance(C, torch.Tensor) else np.asarray(C)
     # f is kept iff max_k |C[f, k]| over the kept k is < rho or NaN (np.max propagates NaN
     # and NaN >= rho is False).  Blocks of candidates: mx[g] = that max over the kept

@@ -364,6 +364,13 @@ fmx_status fmx_gram_exact_finalize(const int64_t* limbs, const int64_t* counts, 
 int32_t fmx_gram_exact_units_per_date(int64_t A);
 /* Host-side run of the same accumulator over n doubles (test hook; no GPU needed). */
 void fmx_debug_exact_fold(const double* x, int64_t n, int64_t* limbs_out, double* value_out);
+/* The step's greedy prune (builder-defined A19, the host walk of engine.greedy_prune): walk
+ * order[0..n_order); factor f is kept iff max over the kept k of |C[f][k]| is NaN or < rho;
+ * at most top_x kept.  C is the symmetric correlation matrix [F][ldc] on the device; kept
+ * (int32 [top_x or F]) and n_kept (int32 [1]) are device buffers.  F <= 20480. */
+fmx_status fmx_greedy_prune(const double* C, int64_t F, int64_t ldc, const int64_t* order, int64_t n_order,
+                            double rho, int64_t top_x, int32_t* kept, int32_t* n_kept, void* stream);
+
 /* The builder-defined corr_prune selector for J rolling windows in one call:
  * per-date Gram partials of the raw panel X (z-scored with stats [F][D][2] from
  * fmx_cs_moment_stats) for every date any window touches, then per window j the pooled

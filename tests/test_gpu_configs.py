@@ -164,6 +164,31 @@ def test_corr_gram_2000_factors_and_prune(dev):
         assert E.greedy_prune(C, order, rho, top) == OG.greedy_prune(Cref, order, rho, top)
 
 
+@pytest.mark.parametrize("F", [1, 37, 300, 2000])
+def test_greedy_prune_device_vs_oracle(dev, F):
+    """fmx_greedy_prune (the step's prune on the device) == the oracle's greedy walk on
+    symmetric correlation matrices with NaN entries, NaN rows, exact ties with rho and
+    every top_x form (None, 0, small, larger than the zoo)."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F + 7)
+    B = rng.uniform(-1, 1, (F, F))
+    C = (B + B.T) / 2
+    np.fill_diagonal(C, 1.0)
+    C[rng.random((F, F)) < 0.01] = np.nan
+    C = np.triu(C) + np.triu(C, 1).T                     # symmetric bit for bit, NaNs included
+    if F > 2:
+        C[2, :] = np.nan
+        C[:, 2] = np.nan
+        C[0, 1] = C[1, 0] = 0.5                          # a tie with rho = 0.5
+    Cd = torch.as_tensor(C, device=dev)
+    for rho in (0.5, 0.7, 0.95):
+        order = list(rng.permutation(F))
+        for top in (None, 0, 5, F + 3):
+            assert E.greedy_prune(Cd, order, rho, top) == OG.greedy_prune(C, order, rho, top), (rho, top)
+
+
 @pytest.mark.parametrize("F,D,A", [(300, 7, 131), (2000, 4, 96)])
 def test_gram_direct_equals_materialised(dev, F, D, A):
     """The wide Gram straight from the panel (fmx_gram_direct: z-scored while staged from
