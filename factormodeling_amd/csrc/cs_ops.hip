@@ -192,20 +192,22 @@ struct CsrZc {
 };
 constexpr int CSR_ZC_WORDS = 8 * CSR_EL * (CSR_NT / 8) / 32;   // bit words of the longest row
 
-template <int OP>
-__global__ void __launch_bounds__(CSR_NT, OP == FMX_CS_GRAM_Z ? 4 : 8)
+// NT: threads per workgroup (one row each); 256 for rows of <= 32 numpy leaves (the z pass)
+template <int OP, int NT = CSR_NT>
+__global__ void __launch_bounds__(NT, OP == FMX_CS_GRAM_Z ? 4 * NT / NT : 8)
 k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nrows, int64_t A, int64_t ld,
                PwTable pw, int slen, double* __restrict__ stats, double* __restrict__ Y2, int nts, CsrZc zc) {
+  constexpr int ZCW = 8 * CSR_EL * (NT / 8) / 32;           // bit words of the longest row
   __shared__ int32_t sch[PW_LDS_MAX];
-  __shared__ double nodes[2 * (CSR_NT / 8) + 8];
-  __shared__ int iscr[CSR_NT / 64 + 2];
-  __shared__ uint32_t bw[OP == FMX_CS_GRAM_Z ? CSR_ZC_WORDS : 1];
+  __shared__ double nodes[2 * (NT / 8) + 8];
+  __shared__ int iscr[NT / 64 + 2];
+  __shared__ uint32_t bw[OP == FMX_CS_GRAM_Z ? ZCW : 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   {
     const int32_t* g = pw.get((int)A);
-    for (int i = tid; i < slen; i += CSR_NT) sch[i] = g[i];
+    for (int i = tid; i < slen; i += NT) sch[i] = g[i];
     if (OP == FMX_CS_GRAM_Z)
-      for (int i = tid; i < CSR_ZC_WORDS; i += CSR_NT) bw[i] = 0u;
+      for (int i = tid; i < ZCW; i += NT) bw[i] = 0u;
   }
   __syncthreads();
   PwView sv{sch};
@@ -263,11 +265,11 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
     combine();
     if (tid == 0) {
       int tot = 0;
-      for (int w = 0; w < CSR_NT / 64; ++w) tot += iscr[w];
-      iscr[CSR_NT / 64] = tot;
+      for (int w = 0; w < NT / 64; ++w) tot += iscr[w];
+      iscr[NT / 64] = tot;
     }
     __syncthreads();
-    const int cnt = iscr[CSR_NT / 64];
+    const int cnt = iscr[NT / 64];
     const double mean = cnt > 0 ? nodes[0] / (double)cnt : qnan();
     double sd = 0.0;
     if (OP != FMX_CS_MEAN) {
@@ -322,10 +324,10 @@ k_cs_moment_rg(const double* __restrict__ X, double* __restrict__ Y, int64_t nro
           zr[st + q] = ok ? (t - mean) / sd : 0.0;
           if (ok) atomicOr(&bw[(st + q) >> 5], 1u << ((st + q) & 31));
         }
-      for (int64_t a = A + tid; a < zc.apad; a += CSR_NT) zr[a] = 0.0;
+      for (int64_t a = A + tid; a < zc.apad; a += NT) zr[a] = 0.0;
       __syncthreads();
       uint32_t* br = zc.bits + ((row / zc.nd) * zc.nd_all + row % zc.nd) * zc.nwd;
-      for (int w = tid; w < zc.nwd; w += CSR_NT) {
+      for (int w = tid; w < zc.nwd; w += NT) {
         br[w] = bw[w];
         bw[w] = 0u;                                    // the next row's atomics follow the loop-end barrier
       }
@@ -812,16 +814,18 @@ extern "C" fmx_status fmx_cs_moment(int32_t op, const double* X, double* Y, int6
 // validity bits [F][nd_all][nwd] (rows of this chunk).  FMX_ERR_UNSUPPORTED when the row does
 // not fit the register-resident kernel (the caller keeps the stats + tile-kernel z path).
 namespace fmx {
-bool gram_zc_fits(int64_t A) {
-  if (A < 8 || ceil_div(A, (int64_t)32) > CSR_ZC_WORDS) return false;
+// leaves of the numpy schedule of n = A (0: does not fit the register-resident kernel)
+static int gram_zc_leaves(int64_t A) {
+  if (A < 8 || ceil_div(A, (int64_t)32) > CSR_ZC_WORDS) return 0;
   const int slen = pw_len((int)A);
-  if (slen > PW_LDS_MAX) return false;
+  if (slen > PW_LDS_MAX) return 0;
   std::vector<int32_t> sh(slen);
   fmx_debug_pw_schedule((int32_t)A, sh.data(), slen);
   bool fits = sh[1] > 0 && sh[1] <= CSR_NT / 8;
   for (int k = 0; fits && k < sh[1]; ++k) fits = sh[5 + sh[1] + k] <= 8 * CSR_EL;
-  return fits;
+  return fits ? sh[1] : 0;
 }
+bool gram_zc_fits(int64_t A) { return gram_zc_leaves(A) > 0; }
 
 fmx_status gram_zc_pass(const double* X, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t dc0, int64_t ndc,
                         double* Zc, int64_t apad, uint32_t* bits, int64_t nd_all, int64_t nwd, void* stream) {
@@ -831,14 +835,22 @@ fmx_status gram_zc_pass(const double* X, int64_t F, int64_t D, int64_t A, int64_
   PwTable pw = pw_table((int)A, &e);
   if (e) return e;
   int slen = pw_len((int)A);
-  const void* kr = (const void*)k_cs_moment_rg<FMX_CS_GRAM_Z>;
-  static const int64_t slots = [kr] {
+  // rows of <= 32 leaves (A <= ~4096): 256-thread workgroups, every lane holding a leaf's
+  // elements, twice the rows in flight per CU (FMX_GRAM_ZC_NT=512: the A/B arm)
+  static const int want = [] { const char* e = getenv("FMX_GRAM_ZC_NT"); return e ? atoi(e) : 256; }();
+  const bool half = want == 256 && gram_zc_leaves(A) <= 32;
+  const int nt = half ? 256 : CSR_NT;
+  const void* kr = half ? (const void*)k_cs_moment_rg<FMX_CS_GRAM_Z, 256> : (const void*)k_cs_moment_rg<FMX_CS_GRAM_Z>;
+  static int64_t slots_cache[2] = {0, 0};
+  int64_t& slots = slots_cache[half ? 1 : 0];
+  if (!slots) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kr, CSR_NT, 0) != hipSuccess)
-      return (int64_t)256;
-    return (int64_t)std::max(1, per) * std::max(1, cus);
-  }();
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kr, nt, 0) != hipSuccess)
+      slots = 256;
+    else
+      slots = (int64_t)std::max(1, per) * std::max(1, cus);
+  }
   const int64_t nrows = F * ndc;
   FMX_ARG(nrows <= 0x7fffffffll, "too many rows");
   const int64_t grid = std::min<int64_t>(nrows, slots);
@@ -847,7 +859,7 @@ fmx_status gram_zc_pass(const double* X, int64_t F, int64_t D, int64_t A, int64_
   int nts = 0;
   void* rargs[] = {(void*)&X, (void*)&Y, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&pw, (void*)&slen,
                    (void*)&stats, (void*)&Y2, (void*)&nts, (void*)&zc};
-  FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(CSR_NT), rargs, 0, as_stream(stream)));
+  FMX_HIP(hipLaunchKernel(kr, dim3((unsigned)grid), dim3(nt), rargs, 0, as_stream(stream)));
   return FMX_OK;
 }
 }  // namespace fmx
