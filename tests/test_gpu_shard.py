@@ -114,6 +114,28 @@ def test_gram_exact_split_invariant_on_device(dev, F, A):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("F,D,A,d0", [(40, 600, 300, 7), (260, 20, 5000, 0), (24, 40, 9000, 3), (30, 50, 5, 2)])
+def test_gram_direct_exact_row_regimes(dev, F, D, A, d0):
+    """The exact wide Gram across its row regimes: the z pass in 256-thread workgroups (<= 32
+    numpy leaves; 600 dates = two z chunks of 32 date blocks, with a block phase), in
+    512-thread ones (5000 assets), and rows it does not take (> 8192 or < 8 assets: the
+    stats + z-while-staging path with its own stats) -- G and N vs the oracle."""
+    import torch
+    import factormodeling_amd.engine as E
+    import oracle.gram as OG
+    rng = np.random.default_rng(F * A + D)
+    X = rng.standard_normal((F, D, A))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    X[1, d0 + 1] = 0.25                              # constant row: invalid
+    Xd = torch.as_tensor(X, device=dev)
+    L, N = E.gram_direct_exact(Xd, d0, D, d_origin=0)
+    G, Nf = E.gram_exact_finalize(L, N)
+    Z, M = OG.zscore_exposures(X[:, d0:])
+    Zf, Mf = Z.reshape(F, -1), M.reshape(F, -1)
+    np.testing.assert_allclose(G.cpu().numpy(), Zf @ Zf.T, rtol=1e-11, atol=1e-9)
+    assert np.array_equal(Nf.cpu().numpy(), Mf @ Mf.T)
+
+
 @pytest.mark.parametrize("F,A", [(300, 257), (520, 1000)])
 def test_gram_direct_exact_block_split_invariant(dev, F, A):
     """fmx_gram_direct_exact (the wide Gram): any split of the dates at
