@@ -496,6 +496,9 @@ __host__ __device__ inline int64_t unit_chunk(int64_t u, int S, int64_t nch) {
   return (u / S) * nch + ((u % S) * nch) / S;
 }
 
+#ifndef GDB_PAD
+#define GDB_PAD 1      // k_gram_db k-steps without the per-block branch (dummy block for short waves; 0: A/B arm, +0.4 ms at C2)
+#endif
 template <int NB, bool ZIN, bool UNITS = false>   // ZIN: X holds the z-scores (cs_zscore output), stats unused
 __global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
@@ -611,8 +614,15 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
       const int kk = ks + (lane >> 4);
 #pragma unroll
       for (int u = 0; u < BPW; ++u) {
+#if GDB_PAD
+        // no branch: a wave short of BPW blocks multiplies block 0 again into the unused
+        // accumulator (never stored), so the k-step is straight-line code
+        const int bk = blk[u] < 0 ? blk[0] : blk[u];
+#else
         if (blk[u] < 0) continue;                 // wave-uniform
-        const int bi = blk[u] & 0xff, bj = blk[u] >> 8;
+        const int bk = blk[u];
+#endif
+        const int bi = bk & 0xff, bj = bk >> 8;
         const double a = Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
         const double bb = Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
         gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
