@@ -8,7 +8,8 @@ between date shards, behind one small interface so the same step code runs over
   (halo send/recv, IC all-gather, exact Gram all-reduce) runs on the HIP kernels of a
   single MI355X and can be compared bit-for-bit with the 1-shard run.
 
-Exchanges: point-to-point halo slabs to rank+1 (``isend``/``irecv``),
+Exchanges: point-to-point halo slabs to rank+1 (``exchange``: one
+``batch_isend_irecv`` group of the rank's send and receive),
 the daily IC series (``all_gather``) and the exact Gram limbs / pair counts
 (``all_reduce_sum`` of int64 -- integer sums, so the reduction order is free).
 """
@@ -32,6 +33,13 @@ class TorchComm:
 
     def irecv(self, t, src):
         return dist.irecv(t, src)
+
+    def exchange(self, sends, recvs):
+        """Point-to-point sends [(t, dst)] and receives [(t, src)] posted as ONE
+        ``batch_isend_irecv`` group (RCCL coalesces the group's transfers); the returned
+        requests are waited on by the caller."""
+        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends] + [dist.P2POp(dist.irecv, t, s) for t, s in recvs]
+        return dist.batch_isend_irecv(ops) if ops else []
 
     def all_gather(self, t):
         parts = [torch.empty_like(t) for _ in range(self.world)]
@@ -141,6 +149,9 @@ class LocalComm:
 
     def irecv(self, t, src):
         return _Recv(self.hub, self._key(src, self.rank), t)
+
+    def exchange(self, sends, recvs):
+        return [self.isend(t, d) for t, d in sends] + [self.irecv(t, s) for t, s in recvs]
 
     def all_gather(self, t):
         return self.hub.gather(self.rank, t.contiguous())

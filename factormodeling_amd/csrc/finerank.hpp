@@ -357,7 +357,9 @@ __device__ __forceinline__ void fr_park_sample(FrTab& T, const uint64_t* key) {
   }
 }
 
-template <int K, int G>
+// EQB: an equal-to-sample bucket id also carries FR_BEQ (callers mask it off for the counter)
+constexpr int FR_BEQ = 1 << 16;
+template <int K, int G, bool EQB = false>
 __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* key, int* b, int dummy) {
   int i[G];
   uint64_t last[G];                           // largest sample <= key
@@ -393,7 +395,7 @@ __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* ke
   for (int k = 0; k < G; ++k) {
     const double tt = (okey_inv(key[k]) - li[k].x) * li[k].y;
     const int sub = li[k].y > 0.0 ? (int)fmin(tt, (double)(K - 1)) : 0;
-    const int be = (i[k] - 1) * (K + 1) + K, bf = i[k] * (K + 1) + sub;
+    const int be = ((i[k] - 1) * (K + 1) + K) | (EQB ? FR_BEQ : 0), bf = i[k] * (K + 1) + sub;
     // a sentinel key (> every real key) only matches sentinel padding: dummy either way
     b[k] = key[k] == KEY_SENTINEL ? dummy : (last[k] == key[k] ? be : bf);
   }
@@ -404,13 +406,13 @@ __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* ke
 // bucket `dummy`.
 // G: group size (fewer keys in flight for register-tight launches, e.g. 1024-thread rows
 // at 64 VGPRs)
-template <int K, int EMAX, int G = 4>
+template <int K, int EMAX, int G = 4, bool EQB = false>
 __device__ __forceinline__ void fr_bucket_all(const FrTab& T, const uint64_t* key, int* b, int dummy) {
   if constexpr (EMAX <= G + 1) {
-    fr_bucket_grp<K, EMAX>(T, key, b, dummy);
+    fr_bucket_grp<K, EMAX, EQB>(T, key, b, dummy);
   } else {
-    fr_bucket_grp<K, G>(T, key, b, dummy);
-    fr_bucket_all<K, EMAX - G, G>(T, key + G, b + G, dummy);
+    fr_bucket_grp<K, G, EQB>(T, key, b, dummy);
+    fr_bucket_all<K, EMAX - G, G, EQB>(T, key + G, b + G, dummy);
   }
 }
 
@@ -434,6 +436,14 @@ __device__ __forceinline__ uint32_t fr_cnt_add(uint32_t* w, int b) {
 }
 __device__ __forceinline__ uint32_t fr_cnt_get(const uint32_t* w, int b) {
   return (w[b >> 1] >> ((b & 1) << 4)) & 0xffffu;
+}
+// Counters b and b + 1 (after the scan: the bucket's start and end) from one ds_read2.
+__device__ __forceinline__ void fr_cnt_get2(const uint32_t* w, int b, int* s0, int* s1) {
+  const uint32_t* p = w + (b >> 1);
+  const uint32_t w0 = p[0], w1 = p[1];
+  const bool odd = b & 1;
+  *s0 = (int)(odd ? (w0 >> 16) : (w0 & 0xffffu));
+  *s1 = (int)(odd ? (w1 & 0xffffu) : (w0 >> 16));
 }
 
 // In-place exclusive scan of WORDS packed 16-bit counters (2 per word, 16-byte aligned),
@@ -479,6 +489,121 @@ __device__ void fr_scan16(uint32_t* w, int* scr) {
     v[j] = o;
   }
   __syncthreads();
+}
+
+// ---- List-balanced in-bucket scans ---------------------------------------------------
+// An element sharing a fine bucket with other, distinct keys needs #less / #equal among the
+// bucket's n members.  Scanned by its owning lane (one exec-masked loop per element slot),
+// a wave pays max-over-lanes(n) iterations per slot while only ~40 % of its lanes have work
+// (C5's ranks-only pass spent 42 % of its time there).  Instead every such element becomes
+// a 32-bit work item (bucket start | slot << 16 | n << 24) in an LDS list that all threads
+// walk, and the result (#less | #equal << 16) replaces the item.  Two kinds of item:
+// pairs (n = 2: one compare with the other member, no loop) fill the list from the front,
+// larger buckets (n <= 255) from the back, so consecutive items have similar work.  Index
+// claims are ballot prefix counts per wave (no atomics); items past the list's capacity or
+// with n > 255 are scanned by their owner (FR_SELF).
+constexpr int FR_SELF = (int)0x80000000u;
+
+struct FrClaim {
+  int a = 0, b = 0;          // the wave's pair / multi items so far (wave-uniform)
+};
+// ref: slot | kind << 8 | index-in-wave << 10 (kind 0 pair, 1 multi), or slot | FR_SELF.
+__device__ __forceinline__ int fr_claim(FrClaim& c, bool scan, int n, int slot) {
+  const bool pa = scan && n == 2, pb = scan && (unsigned)(n - 3) <= 252u;
+  const uint64_t ma = __builtin_amdgcn_ballot_w64(pa), mb = __builtin_amdgcn_ballot_w64(pb);
+  // (a select of the whole mask and a ternary ref: the branch-free forms of both made the
+  // compiler spill in the 80- and 128-VGPR rank kernels)
+  const uint64_t m = pa ? ma : mb;
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int idx = (pa ? c.a : c.b) + below;
+  c.a += __popcll(ma);
+  c.b += __popcll(mb);
+  return pa ? (slot | idx << 10) : (pb ? (slot | 1 << 8 | idx << 10) : (slot | FR_SELF));
+}
+// After every slot's claim: lane 0 parks the wave's totals (wtot: NT/64 entries).
+__device__ __forceinline__ void fr_claim_publish(int2* wtot, const FrClaim& c) {
+  if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = make_int2(c.a, c.b);
+}
+// After a barrier: the wave's bases and the list's occupancy (pairs [0, na), multis
+// [cap - nb, cap)).
+struct FrListBase {
+  int a0, b0, na, nb, cap;
+  template <int NW>
+  __device__ __forceinline__ static FrListBase make(const int2* wtot, int cap_) {
+    FrListBase r;
+    r.init<NW>(wtot, cap_);
+    return r;
+  }
+  template <int NW>
+  __device__ __forceinline__ void init(const int2* wtot, int cap_) {
+    const int wid = threadIdx.x >> 6;
+    int ta = 0, tb = 0;
+    a0 = b0 = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int2 v = wtot[w];
+      a0 += w < wid ? v.x : 0;
+      b0 += w < wid ? v.y : 0;
+      ta += v.x;
+      tb += v.y;
+    }
+    cap = cap_;
+    na = ta < cap ? ta : cap;
+    nb = tb < cap - na ? tb : cap - na;
+  }
+};
+// Scatter of a scanned element: its key into the bucket range, its work item into the
+// list.  Returns the list index, or slot | FR_SELF when its owner scans it.
+__device__ __forceinline__ int fr_list_put(uint64_t* bkey, uint32_t* items, const FrListBase& lb, int ref, int s0,
+                                           int n, uint64_t key) {
+  const bool self = ref < 0;
+  const int slot = self ? (ref & 0x3fff) : (ref & 0xff);
+  bkey[s0 + slot] = key;
+  if (self) return ref;
+  const int idx = ref >> 10;
+  const bool multi = (ref >> 8) & 1;
+  const int g = multi ? lb.cap - 1 - (lb.b0 + idx) : lb.a0 + idx;
+  const bool ok = multi ? g >= lb.cap - lb.nb : g < lb.na;
+  if (!ok) return slot | FR_SELF;
+  items[g] = (uint32_t)s0 | ((uint32_t)slot << 16) | ((uint32_t)n << 24);
+  return g;
+}
+// Every thread: walk the list, result #less | #equal << 16 in place of each item.
+template <int NT>
+__device__ __forceinline__ void fr_list_walk(const uint64_t* bkey, uint32_t* items, const FrListBase& lb) {
+  for (int g = threadIdx.x; g < lb.na; g += NT) {            // pairs: one compare
+    const uint32_t it = items[g];
+    const uint64_t* bk = bkey + (it & 0xffffu);
+    const int slot = (int)((it >> 16) & 1u);
+    const uint64_t own = bk[slot], oth = bk[slot ^ 1];
+    items[g] = (uint32_t)((oth < own ? 1 : 0) + (oth == own ? 0x20000 : 0x10000));
+  }
+  for (int g = lb.cap - lb.nb + (int)threadIdx.x; g < lb.cap; g += NT) {
+    const uint32_t it = items[g];
+    const uint64_t* bk = bkey + (it & 0xffffu);
+    const int slot = (int)((it >> 16) & 0xffu), n = (int)(it >> 24);
+    const uint64_t own = bk[slot];
+    int acc = 0;
+    for (int j = 0; j < n; ++j) {
+      const uint64_t w = bk[j];
+      acc += (w < own ? 1 : 0) + (w == own ? 0x10000 : 0);
+    }
+    items[g] = (uint32_t)acc;
+  }
+}
+// Owner scan of an element the list did not take: #less | #equal << 16.
+__device__ __forceinline__ int fr_self_scan(const uint64_t* bk, int n, uint64_t own) {
+  int acc = 0;
+  for (int j = 0; j < n; ++j) {
+    const uint64_t w = bk[j];
+    acc += (w < own ? 1 : 0) + (w == own ? 0x10000 : 0);
+  }
+  return acc;
+}
+// Byte offset of the list behind the keys / counters (16-byte aligned).
+__host__ __device__ inline int64_t fr_list_off(int64_t A, int64_t words) {
+  const int64_t b = A * 8 > words * 4 ? A * 8 : words * 4;
+  return (b + 15) / 16 * 16;
 }
 
 // In-place exclusive scan of c[0..n) with c[n] = total, by a block of NT threads (each

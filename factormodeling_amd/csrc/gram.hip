@@ -615,9 +615,10 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
 #pragma unroll
       for (int u = 0; u < BPW; ++u) {
 #if GDB_PAD
-        // no branch: a wave short of BPW blocks multiplies block 0 again into the unused
-        // accumulator (never stored), so the k-step is straight-line code
-        const int bk = blk[u] < 0 ? blk[0] : blk[u];
+        // no branch: a wave short of BPW blocks multiplies block (0, 0) -- which always
+        // exists -- into the unused accumulator (never stored), so the k-step is
+        // straight-line code (a wave owning no block at all, NTRI < waves, does the same)
+        const int bk = blk[u] < 0 ? 0 : blk[u];
 #else
         if (blk[u] < 0) continue;                 // wave-uniform
         const int bk = blk[u];
@@ -2094,7 +2095,7 @@ extern "C" fmx_status fmx_gram_direct(const double* X, const double* stats, doub
 // FMX_GRAM_ZC=0 keeps the stats + z-while-staging form): the dates run in chunks of
 // zc_slices date blocks -- a z pass (row moments, Zc, validity bits) then the tile kernel on
 // Zc with no staging arithmetic.  32 blocks of C4's 72 tiles make 9 full rounds of the CUs;
-// the Zc chunk is capped at 32 GB.
+// the Zc chunk is capped at 32 GB (FMX_GRAM_ZC_GB).
 static bool gram_zc_enabled(int64_t A) {
   static const int on = [] { const char* e = getenv("FMX_GRAM_ZC"); return e ? atoi(e) : 1; }();
   return on && gram_zc_fits(A);
@@ -2114,7 +2115,12 @@ static DirectPlan direct_exact_plan(int64_t F, int64_t D, int64_t A, int64_t d0,
   if (zc) {
     p.apad = ceil_div(A, (int64_t)GW_K) * GW_K;
     const int64_t per_slice = (int64_t)sizeof(double) * F * FMX_GRAM_DATE_BLOCK * p.apad;
-    p.zc_slices = std::max<int64_t>(1, std::min<int64_t>({(int64_t)32, p.g.nslice, ((int64_t)32 << 30) / per_slice}));
+    // FMX_GRAM_ZC_GB (read per call): a smaller cap for runs that hold several shards'
+    // workspaces on one device at once (the in-process 8-shard test); the blocks' exact
+    // partials do not depend on the chunking
+    const char* cap_e = getenv("FMX_GRAM_ZC_GB");
+    const int64_t cap_gb = cap_e && atoi(cap_e) > 0 ? atoi(cap_e) : 32;
+    p.zc_slices = std::max<int64_t>(1, std::min<int64_t>({(int64_t)32, p.g.nslice, (cap_gb << 30) / per_slice}));
   }
   return p;
 }

@@ -29,12 +29,14 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   fmx_rank2_t* RK = nullptr;
   FrIc ic{};
   FrZn zn{};
+  const FrListLds ll = fr_list_lds(kfr, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
+  int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
-  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
-  FMX_HIP(hipLaunchKernel(kfr, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(hipLaunchKernel(kfr, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -53,10 +55,12 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   int method = FMX_RANK_AVERAGE;
   FrIc ic{};
   FrZn zn{};
+  const FrListLds ll = fr_list_lds(k, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
+  int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
-  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
+  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -77,10 +81,13 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
   const uint8_t* present = nullptr;
   FrIc ic{};
   FrZn zn{Yz, Yn, pw, slen};
+  // the moments' scratch sits where the scan list goes later
+  const FrListLds ll = fr_list_lds(k, A, (size_t)fr_list_off(A, FR_CS_WORDS), FR_ZN_SCR_BYTES);
+  int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
-  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
+  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -102,8 +109,11 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   const int E = br_emax(A, nt_fa);
   if (nt_fa == 1024 && E == 10 && rank_impl() == RANK_IMPL_FINE && rank2_pf_enabled()) {
     int64_t nrows = F * D;
-    void* args[] = {(void*)&X, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&RK};
-    return launch_persistent((const void*)k_cs_rank2_pf<1024, 10>, 1024, nrows, lds_fr, args, st);
+    const void* kp = (const void*)k_cs_rank2_pf<1024, 10>;
+    const FrListLds ll = fr_list_lds(kp, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
+    int lcap = ll.cap;
+    void* args[] = {(void*)&X, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&RK, (void*)&lcap};
+    return launch_persistent(kp, 1024, nrows, ll.bytes, args, st);
   }
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense)(nt_fa, E);
   if (!k || !lds_fits(k, lds_fr)) { set_error("fmx_cs_rank2: A <= 16384"); return FMX_ERR_UNSUPPORTED; }
@@ -116,10 +126,12 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   double qlo = 0.0, qhi = 0.0;
   FrIc ic{};
   FrZn zn{};
+  const FrListLds ll = fr_list_lds(k, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
+  int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn};
-  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
+  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 

@@ -81,6 +81,8 @@ struct FrZn {
   int slen;                  // its length in int32 words
 };
 constexpr int FR_ZN_NODES = 2 * (16384 / 64) + 8;
+// the moments' scratch (schedule + tree nodes) aliases the scan list: bytes it needs there
+constexpr int FR_ZN_SCR_BYTES = PW_LDS_MAX * 4 + FR_ZN_NODES * 8;
 constexpr int FR_IC_EC = 256;  // E entries per lag held in LDS; longer lists: ovf
 #ifndef FR_IC_CH
 #define FR_IC_CH 2             // return loads in flight per thread in the IC pass
@@ -366,22 +368,26 @@ template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false, bool ZN
 __global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
-             fmx_rank2_t* __restrict__ RK, FrIc ic, FrZn zn) {
+             fmx_rank2_t* __restrict__ RK, FrIc ic, FrZn zn, int lcap) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;   // sentinel bucket: last half-word
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
   __shared__ FrTab tab;
   __shared__ uint4 wred[NW];                  // per wave: #present, #valid, min / max key high words
   __shared__ int iscr[NW];
-  extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters)
+  __shared__ int2 lwt[NW];                    // in-bucket scan list: per-wave claim totals
+  // dynamic: max(A keys, WORDS packed counters), then the scan list (lcap items; with ZN the
+  // moments' schedule and tree nodes alias it)
+  extern __shared__ uint64_t lds[];
   uint32_t* cnt = (uint32_t*)lds;             // 16-bit counter of bucket b: half b & 1 of word b >> 1
   uint64_t* bkey = lds;
+  uint32_t* litems = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + fr_list_off(A, WORDS));
   const int t = threadIdx.x, wid = t >> 6;
   BR_PH_INIT;
   static_assert(!(IC && PRES), "the fused IC ranks dense rows");
   static_assert(!ZN || (WQ && !PRES && !IC), "ZN: dense rank + winsor rows");
-  __shared__ int32_t zn_sch[ZN ? PW_LDS_MAX : 1];
-  __shared__ double zn_nodes[ZN ? FR_ZN_NODES : 1];
+  int32_t* zn_sch = reinterpret_cast<int32_t*>(litems);
+  double* zn_nodes = reinterpret_cast<double*>(litems + PW_LDS_MAX);
   __shared__ int zn_iscr[ZN ? NW + 2 : 1];
   FrIcRow rw{};
   __shared__ int ic_ne[2];                    // E-list lengths (IC)
@@ -435,6 +441,10 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       for (int i = t; i < zn.slen; i += NT) zn_sch[i] = g[i];
     __syncthreads();
     const int32_t* sch = sl ? zn_sch : g;
+#ifdef FR_DIAG_NOZNSUM
+    int cnt = An; (void)sch;
+    const double s1 = vrow[t], mean = s1, s2 = vrow[t + 1], var = s2;
+#else
     int cnt, c2;
     const double s1 = block_pw_sum_w0<NT>([&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; },
                                           [&](int i) { return (int)(vrow[i] == vrow[i]); }, sch, zn_nodes,
@@ -447,6 +457,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       return u == u ? q : 0.0;
     }, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
     const double var = cnt > 0 ? s2 / (double)cnt : qnan();
+#endif
     const double sd = sqrt(var);
     const bool g2 = sd == 0.0 || sd != sd;     // neutralize: sigma in {0, NaN} -> 0
     double* yz = zn.Yz + row * ld;
@@ -523,69 +534,55 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   int sl[EMAX];                               // slot | bucket << PK_BSHIFT, then start | len << 16
   {
     int bb[EMAX];
-    fr_bucket_all<K, EMAX, (NT >= 1024 ? 2 : 4)>(tab, key, bb, DUMMY);
+    fr_bucket_all<K, EMAX, (NT >= 1024 ? 2 : 4), true>(tab, key, bb, DUMMY);
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) sl[k] = (int)fr_cnt_add(cnt, bb[k]) | (bb[k] << PK_BSHIFT);
+    for (int k = 0; k < EMAX; ++k) sl[k] = (int)fr_cnt_add(cnt, bb[k] & (FR_BEQ - 1)) | (bb[k] << PK_BSHIFT);
   }
   __syncthreads();
   fr_scan16<NT, WORDS>(cnt, iscr);
   BR_PH();
-  // le[k] = #less | #equal << 16 inside the bucket (for elements still to scan: their
-  // scatter slot until the scatter is done)
+  // le[k] = #less | #equal << 16 inside the bucket; for elements still to scan (n field of
+  // sl set) first their list claim (fr_list_claim), then their list index or slot | FR_SELF
   int le[EMAX];
+  FrClaim lcl;
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) {
-    const int b = sl[k] >> PK_BSHIFT;
+    const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
     const int slot = sl[k] & PK_SLOT;
-    const int s0 = (int)fr_cnt_get(cnt, b);
-    const int n = (int)fr_cnt_get(cnt, b + 1) - s0;
-    const bool eqb = (b % (K + 1)) == K;      // equal-to-sample bucket: all members tie
+    int s0, s1;
+    fr_cnt_get2(cnt, b, &s0, &s1);
+    const int n = s1 - s0;
+    const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
     const bool scan = !eqb && n > 1 && b != DUMMY;
-    le[k] = scan ? slot : (eqb ? n : 1) << 16;
+    const int ref = fr_claim(lcl, scan, n, slot);
+    le[k] = scan ? ref : (eqb ? n : 1) << 16;
     sl[k] = s0 | (scan ? n << 16 : 0);
+    FR_SCHED_FENCE();
   }
+  fr_claim_publish(lwt, lcl);
   __syncthreads();                            // counters dead: the keys reuse their LDS
-  int maxlen = 0;
-#pragma unroll
-  for (int k = 0; k < EMAX; ++k) {
-    const int n = sl[k] >> 16;
-    if (n) {
-      bkey[(sl[k] & 0xffff) + le[k]] = key[k];
-      le[k] = 0;
-    }
-    maxlen = max(maxlen, n);
-  }
-  __syncthreads();
-  BR_PH();
-#if FR_SCAN_PERK
-  // one exec-masked loop per element slot: a wave runs sum_k max_lanes(n_k) short
-  // iterations instead of max_lanes max_k(n_k) iterations over all EMAX slots
-  (void)maxlen;
-#pragma unroll
-  for (int k = 0; k < EMAX; ++k) {
-    const int n = sl[k] >> 16;
-    if (n) {
-      const uint64_t* bk = bkey + (sl[k] & 0xffff);
-      const uint64_t own = key[k];
-      int acc = 0;
-      for (int j = 0; j < n; ++j) {
-        const uint64_t w = bk[j];
-        acc += (w < own ? 1 : 0) + (w == own ? 0x10000 : 0);
-      }
-      le[k] = acc;
-    }
-  }
-#else
-  for (int j = 0; j < maxlen; ++j) {
+  {
+    const FrListBase lb = FrListBase::make<NW>(lwt, lcap);
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      if (j < (sl[k] >> 16)) {                // exec-masked: idle lanes cost no LDS
-        const uint64_t w = bkey[(sl[k] & 0xffff) + j];
-        le[k] += (w < key[k] ? 1 : 0) + (w == key[k] ? 0x10000 : 0);
+      const int n = sl[k] >> 16;
+      if (n) le[k] = fr_list_put(bkey, litems, lb, le[k], sl[k] & 0xffff, n, key[k]);
+    }
+    __syncthreads();
+    BR_PH();
+#ifndef FR_DIAG_NOSCAN
+    fr_list_walk<NT>(bkey, litems, lb);
+#endif
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int n = sl[k] >> 16;
+      if (n) {
+        const uint64_t* bk = bkey + (sl[k] & 0xffff);
+        le[k] = le[k] >= 0 ? (int)litems[le[k]] : fr_self_scan(bk, n, bk[le[k] & 0x3fff]);
       }
     }
   }
-#endif
   const double den = (double)(nrow - 1);
   const double rden = 1.0 / den;              // (r - 1) / den through mdiv: bit-identical
   // winsor order statistics (numpy linear) of the nv valid keys
@@ -697,9 +694,9 @@ __device__ __forceinline__ void fr_bucket_cnt(const FrTab& T, const uint64_t* ke
                                               uint32_t* cnt) {
   constexpr int g = EMAX < G ? EMAX : G;
   int b[g];
-  fr_bucket_grp<K, g>(T, key, b, dummy);
+  fr_bucket_grp<K, g, true>(T, key, b, dummy);
 #pragma unroll
-  for (int k = 0; k < g; ++k) sl[k] = (int)fr_cnt_add(cnt, b[k]) | (b[k] << PK_BSHIFT);
+  for (int k = 0; k < g; ++k) sl[k] = (int)fr_cnt_add(cnt, b[k] & (FR_BEQ - 1)) | (b[k] << PK_BSHIFT);
   FR_SCHED_FENCE();
   if constexpr (EMAX > G) fr_bucket_cnt<K, EMAX - G, G>(T, key + G, sl + G, dummy, cnt);
 }
@@ -716,24 +713,29 @@ __device__ __forceinline__ void fr_bucket_cnt(const FrTab& T, const uint64_t* ke
 //   rank2 = 2 * #less + #equal + 1 (0 for NaN); single-asset rows -> 2.
 template <int NT, int EMAX>
 __global__ void __launch_bounds__(NT, 4)
-k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld, fmx_rank2_t* __restrict__ RK) {
+k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld, fmx_rank2_t* __restrict__ RK,
+              int lcap) {
   constexpr int K = FR_K_CS, NW = NT / 64;
   constexpr int WORDS = FR_CS_WORDS, DUMMY = 2 * WORDS - 1;
   static_assert(FRG<K>::NB + 1 < DUMMY, "counter array");
   __shared__ FrTab tab;
   __shared__ uint4 wred[NW];
   __shared__ int iscr[NW];
-  extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters)
+  __shared__ int2 lwt[NW];
+  extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters), then the scan list
   uint32_t* cnt = (uint32_t*)lds;
   uint64_t* bkey = lds;
+  uint32_t* litems = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + fr_list_off(A, WORDS));
   const int t = threadIdx.x, wid = t >> 6;
   const int An = (int)A;
+  BR_PH_INIT;
   double xv[EMAX];
   int64_t row = blockIdx.x;
   if (row >= nrows) return;
 #pragma unroll
   for (int k = 0; k < EMAX; ++k) xv[k] = X[row * ld + (fr_ix<NT>(fr_opaque(t), k, (int)A))];
   for (; row < nrows; row += gridDim.x) {
+    BR_PH_ROW();
     uint64_t key[EMAX];
     uint32_t hmin = 0xffffffffu, hmax = 0u;
     int wv = 0;
@@ -753,8 +755,10 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       for (int k = 0; k < EMAX; ++k) xv[k] = X[nxt * ld + (fr_ix<NT>(fr_opaque(t), k, (int)A))];
     }
     fr_park_sample<NT, EMAX>(tab, key);
+    BR_PH();
     __syncthreads();                          // the previous row's scan reads of bkey are done
-#pragma unroll
+    BR_PH();
+  #pragma unroll
     for (int j = 0; j < WORDS / (4 * NT); ++j)
       reinterpret_cast<uint4*>(cnt)[t * (WORDS / (4 * NT)) + j] = make_uint4(0u, 0u, 0u, 0u);
     {
@@ -762,6 +766,7 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       if ((t & 63) == 0) wred[wid] = make_uint4(0u, (uint32_t)wv, a, c);
     }
     __syncthreads();
+    BR_PH();
     int nv = 0;
     uint32_t h0 = 0xffffffffu, h1 = 0u;
 #pragma unroll
@@ -784,42 +789,54 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
     }
     __syncthreads();
+    BR_PH();
     int sl[EMAX];
     fr_bucket_cnt<K, EMAX, 4>(tab, key, sl, DUMMY, cnt);
     __syncthreads();
+    BR_PH();
     fr_scan16<NT, WORDS>(cnt, iscr);
-    int le[EMAX];                             // scatter slot, then c = 2 #less + #equal in the bucket
+    BR_PH();
+    int le[EMAX];                             // list claim / index, then c = 2 #less + #equal in the bucket
     uint32_t nan_m = 0;
+    FrClaim lcl;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      const int b = sl[k] >> PK_BSHIFT;
+      const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
       const int slot = sl[k] & PK_SLOT;
-      const int s0 = (int)fr_cnt_get(cnt, b);
-      const int n = (int)fr_cnt_get(cnt, b + 1) - s0;
-      const bool eqb = (b % (K + 1)) == K;    // equal-to-sample bucket: all members tie
+      int s0, s1;
+      fr_cnt_get2(cnt, b, &s0, &s1);
+      const int n = s1 - s0;
+      const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
       const bool scan = !eqb && n > 1 && b != DUMMY;
       nan_m |= (uint32_t)(b == DUMMY) << k;
-      le[k] = scan ? slot : (eqb ? n : 1);
+      const int ref = fr_claim(lcl, scan, n, slot);
+      le[k] = scan ? ref : (eqb ? n : 1);
       sl[k] = s0 | (scan ? n << 16 : 0);
+      FR_SCHED_FENCE();
     }
+    fr_claim_publish(lwt, lcl);
     __syncthreads();                          // counters dead: the keys reuse their LDS
+    BR_PH();
+    const FrListBase lb = FrListBase::make<NW>(lwt, lcap);
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k)
-      if (sl[k] >> 16) bkey[(sl[k] & 0xffff) + le[k]] = key[k];
+    for (int k = 0; k < EMAX; ++k) {
+      const int n = sl[k] >> 16;
+      if (n) le[k] = fr_list_put(bkey, litems, lb, le[k], sl[k] & 0xffff, n, key[k]);
+    }
     __syncthreads();
+    BR_PH();
+#ifndef FR_DIAG_NOSCAN
+    fr_list_walk<NT>(bkey, litems, lb);
+#endif
+    __syncthreads();
+    BR_PH();
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       const int n = sl[k] >> 16;
       if (n) {
         const uint64_t* bk = bkey + (sl[k] & 0xffff);
-        const uint64_t own = bk[le[k]];       // own key from its slot: keys dead after the scatter
-        int c = 0;
-#pragma unroll 2
-        for (int j = 0; j < n; ++j) {
-          const uint64_t w = bk[j];
-          c += (w < own ? 2 : 0) + (w == own ? 1 : 0);
-        }
-        le[k] = c;
+        const int c = le[k] >= 0 ? (int)litems[le[k]] : fr_self_scan(bk, n, bk[le[k] & 0x3fff]);
+        le[k] = 2 * (c & 0xffff) + (c >> 16);
       }
     }
 #pragma unroll
@@ -828,6 +845,7 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       const uint32_t r2 = ((nan_m >> k) & 1u) ? 0u : (uint32_t)(2 * (sl[k] & 0xffff) + le[k] + 1);
       __builtin_nontemporal_store((fmx_rank2_t)r2, rk + fr_opaque(t) + k * NT);
     }
+    BR_PH();
   }
 }
 

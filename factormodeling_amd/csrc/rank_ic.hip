@@ -472,10 +472,14 @@ fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const d
   int method = FMX_RANK_AVERAGE;
   const uint8_t* present = nullptr;
   fmx_rank2_t* RKrow = nullptr;
+  // the IC tail's LDS (from 0) outlives the scan list behind the keys / counters
+  const size_t loff = (size_t)fr_list_off(A, FR_CS_WORDS);
+  const FrListLds ll = fr_list_lds(k, A, loff, lds_fr > loff ? lds_fr - loff : 0);
+  int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic, (void*)&zn};
-  if (lds_fr > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fr));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, lds_fr, st));
+                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic, (void*)&zn, (void*)&lcap};
+  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
   static const int list_grid = [] {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -46,6 +46,34 @@ static inline bool lds_fits(const void* k, size_t dyn) {
   return at.sharedSizeBytes + dyn <= 160 * 1024;
 }
 
+// Dynamic LDS of a fine-bucket rank launch with its in-bucket scan list (finerank.hpp
+// fr_list_*): `base` bytes before the list (keys / counters, fr_list_off), then the list.  The
+// capacity is as many 4-byte items as fit without lowering the rows per CU that the launch
+// has without a list (static LDS + base + `extra`, the bytes other phases keep behind base),
+// at most A: a row with more scanned elements than that scans the rest from their owners.
+struct FrListLds {
+  int cap;
+  size_t bytes;
+};
+static inline FrListLds fr_list_lds(const void* k, int64_t A, size_t base, size_t extra) {
+  hipFuncAttributes at;
+  size_t stat = 0;
+  if (k && hipFuncGetAttributes(&at, k) == hipSuccess) stat = at.sharedSizeBytes;
+  // per-workgroup LDS is allocated in granules (2 KiB assumed: LDS_Block_Size reports
+  // multiples of it), so the rows per CU are counted on rounded sizes
+  const size_t cu = 160 * 1024, gran = 2048;
+  auto up = [&](size_t b) { return (b + gran - 1) / gran * gran; };
+  const size_t need = up(stat + base + extra);
+  const size_t rows = std::max<size_t>(1, cu / std::max<size_t>(need, 1));
+  const size_t per = cu / rows / gran * gran;
+  const size_t room = per > stat + base ? per - stat - base : 0;
+  const int64_t cap = std::min<int64_t>(A, (int64_t)(room / 4) & ~3ll);
+  FrListLds r;
+  r.cap = (int)std::max<int64_t>(cap, 0);
+  r.bytes = base + std::max<size_t>((size_t)r.cap * 4, extra);
+  return r;
+}
+
 template <class K>
 static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblocks, size_t lds, void** args,
                                    hipStream_t st) {

@@ -94,6 +94,11 @@ def ts_corr(X, Ycol, window: int, present=None, out=None):
     return out
 
 
+# fmx_ts_corr_feature keeps the window's reciprocal table in LDS up to this window
+# (ts_ops.hip TSC_MAXW); longer windows take ts_corr + corr_vol_feature
+CORR_FEATURE_MAX_W = 4096
+
+
 def corr_feature(X, Ycol, window: int, out=None, corr_out=None):
     """C5's feature sign(ts_corr(X, Ycol, window)) * (X / ts_std(X, window)) in one pass
     (fmx_ts_corr_feature): bit-identical to ts_corr + corr_vol_feature, without the corr
@@ -686,7 +691,10 @@ def _greedy_prune_device(C, order, rho, top_x):
         ordt = torch.as_tensor(np.asarray(order, dtype=np.int64), device=C.device)
     # the host walk returns once len(kept) >= top_x after an append: top_x <= 0 keeps one
     lim = F if top_x is None else max(int(top_x), 1)
-    kept = torch.empty(max(min(lim, F), 1), dtype=torch.int32, device=C.device)
+    # the walk appends at most one entry per element of ``order`` (a repeated index can be kept
+    # twice, as in the host walk): the bound handed to the kernel is also the buffer's capacity
+    lim = min(lim, max(int(ordt.numel()), 1))
+    kept = torch.empty(lim, dtype=torch.int32, device=C.device)
     nk = torch.zeros(1, dtype=torch.int32, device=C.device)
     call("fmx_greedy_prune", ptr(C), F, F, ptr(ordt), int(ordt.numel()), float(rho), lim, ptr(kept), ptr(nk),
          stream_ptr())

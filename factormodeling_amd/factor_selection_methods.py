@@ -64,7 +64,7 @@ def ledoit_wolf_shrinkage(returns):
     ok = (std[iu[0]] > 0) & (std[iu[1]] > 0)
     corr = sample_cov[iu][ok] / (std[iu[0]][ok] * std[iu[1]][ok])
     mean_corr = np.mean(corr) if corr.size else 0
-    target = mean_corr * np.outer(std, std)
+    target = (mean_corr * std)[:, None] * std[None, :]      # (mean_corr * std_i) * std_j, as the loop
     np.fill_diagonal(target, var)
     d = np.sum((sample_cov - target) ** 2)
     rc = returns - returns.mean(axis=0)

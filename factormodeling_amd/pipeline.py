@@ -173,13 +173,14 @@ def synthetic_panel(D, A, F, device, seed=0, d_lo=0, d_hi=None, halo=0):
 
 
 def shard_bounds(D, world, rank, align=1):
-    """Owned dates [d_lo, d_hi) of ``rank``: contiguous blocks of ceil(D / world) dates,
-    rounded up to a multiple of ``align`` (the wide Gram's absolute date blocks,
-    E.GRAM_DATE_BLOCK: every block then lies on one rank, so its exact partial is the same
-    at any GPU count)."""
-    per = (D + world - 1) // world
-    per = (per + align - 1) // align * align
-    return min(D, rank * per), min(D, (rank + 1) * per)
+    """Owned dates [d_lo, d_hi) of ``rank``: the ceil(D / align) blocks of ``align`` dates
+    (the wide Gram's absolute date blocks, E.GRAM_DATE_BLOCK: every block then lies on one
+    rank, so its exact partial is the same at any GPU count) split as evenly as whole blocks
+    allow -- rank r owns blocks [r nb / world, (r + 1) nb / world) -- so no rank is left
+    without dates while there are at least ``world`` blocks."""
+    nb = (D + align - 1) // align
+    b0, b1 = rank * nb // world, (rank + 1) * nb // world
+    return min(D, b0 * align), min(D, b1 * align)
 
 
 def shard_align(F):
@@ -247,19 +248,21 @@ class ShardedPanel:
         if self.world == 1:
             return None
         H = self.halo_len
-        reqs, bufs = [], []
+        # one slab per direction: the last H owned dates of every factor with the returns
+        # as factor F ([F + 1][H][A]); the rank's send and receive are one p2p group
+        sends, recvs, bufs = [], [], []
         if self.rank + 1 < self.world:
-            send_x = self.X[:, -H:].contiguous()
-            send_r = self.R[-H:].contiguous()
-            bufs += [send_x, send_r]
-            reqs.append(self.comm.isend(send_x, self.rank + 1))
-            reqs.append(self.comm.isend(send_r, self.rank + 1))
+            slab = torch.cat([self.X[:, -H:], self.R[-H:].unsqueeze(0)], dim=0)
+            bufs.append(slab)
+            sends.append((slab, self.rank + 1))
         recv = None
         if self.rank > 0:
-            recv = (torch.empty((self.F, self.halo, self.A), dtype=self.X.dtype, device=self.X.device),
-                    torch.empty((self.halo, self.A), dtype=self.R.dtype, device=self.R.device))
-            reqs.append(self.comm.irecv(recv[0], self.rank - 1))
-            reqs.append(self.comm.irecv(recv[1], self.rank - 1))
+            recv = torch.empty((self.F + 1, self.halo, self.A), dtype=self.X.dtype, device=self.X.device)
+            recvs.append((recv, self.rank - 1))
+        if hasattr(self.comm, "exchange"):
+            reqs = self.comm.exchange(sends, recvs)
+        else:
+            reqs = [self.comm.isend(t, d) for t, d in sends] + [self.comm.irecv(t, s) for t, s in recvs]
         return reqs, recv, bufs
 
     def exchange_halo_finish(self, handle):
@@ -269,8 +272,8 @@ class ShardedPanel:
         for r in reqs:
             r.wait()
         if recv is not None:
-            self.X[:, :self.halo] = recv[0]
-            self.R[:self.halo] = recv[1]
+            self.X[:, :self.halo] = recv[:self.F]
+            self.R[:self.halo] = recv[self.F]
 
     def exchange_halo(self):
         self.exchange_halo_finish(self.exchange_halo_start())
@@ -545,7 +548,8 @@ def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
         for (op, w), buf in zip(cfg.ret_ops, bufs):
             out = buf[: f1 - f0]
             t0 = _ev(timers)
-            if op == "corr_vol" and hasattr(be, "corr_feature_into"):
+            if op == "corr_vol" and hasattr(be, "corr_feature_into") and w <= getattr(
+                    be, "corr_feature_max_w", E.CORR_FEATURE_MAX_W):
                 # one pass: the corr stays in registers (written only when collected)
                 want = collect is not None and collect.get("_factors") is None
                 be.corr_feature_into(Xc, sp.R, w, sp.feature[f0:f1], out if want else None)
@@ -668,13 +672,14 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     t0 = _ev(timers)
     L = len(lags)
     if sp.world > 1:
-        # every rank pads its owned dates to the longest shard (shard_bounds' block length)
-        per = max(hi - lo for lo, hi in (shard_bounds(sp.D, sp.world, r, getattr(sp, "align", 1))
-                                          for r in range(sp.world)))
+        # every rank pads its owned dates to the longest shard; each slice is placed by
+        # its owner's bounds
+        spans = [shard_bounds(sp.D, sp.world, r, getattr(sp, "align", 1)) for r in range(sp.world)]
+        per = max(hi - lo for lo, hi in spans)
         pad = torch.zeros((L, 4, sp.F, per), dtype=daily.dtype, device=daily.device)
         pad[..., :daily.shape[3]] = daily
         parts = sp.comm.all_gather(pad)
-        full = torch.cat(parts, dim=3)[:, :, :, :sp.D].contiguous()
+        full = torch.cat([p[..., :hi - lo] for p, (lo, hi) in zip(parts, spans)], dim=3).contiguous()
     else:
         full = daily.contiguous()
     _rec(timers, "allgather_ic", t0)

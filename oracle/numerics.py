@@ -24,12 +24,18 @@ import numpy as np
 
 PW_BLOCKSIZE = 128
 BUFSIZE = 8192
+# FAST: 1-D sums by numpy's own add.reduce -- the algorithm restated below, pinned to it
+# bit-for-bit by tests/test_oracle_golden.py::test_pairwise_sum_is_numpys_sum.  Set only by
+# the process pools of the full-size checks (tests/oracle_pool.py); off by default.
+FAST = False
 
 
 # --------------------------------------------------------------------------- pairwise sum
 def pairwise_sum(a: np.ndarray) -> np.ndarray:
     """numpy float64 ``a.sum(axis=-1)`` bit-for-bit, vectorised over leading axes."""
     a = np.asarray(a, dtype=np.float64)
+    if FAST and a.ndim == 1:
+        return np.add.reduce(a)
     n = a.shape[-1]
     # the ufunc reduction iterates in buffer-sized chunks (8192 elements) and adds the
     # chunks' pairwise sums sequentially

@@ -61,3 +61,28 @@ def test_corr_feature_vs_oracle(dev):
     got = E.corr_feature(torch.as_tensor(X, device=dev), torch.as_tensor(R, device=dev), 20).cpu().numpy()
     for f in range(F):
         assert_close(got[f].ravel(), O.corr_vol_feature(X[f], R, 20).ravel(), exact=True, what=f"feature f{f}")
+
+
+def test_long_window_takes_two_pass_path(dev):
+    """windows past the fused pass's table (engine.CORR_FEATURE_MAX_W) run
+    ts_corr + corr_vol_feature in the pipeline instead of raising.  The limit is lowered
+    on a backend instance so a small panel crosses it; both paths give the same bits."""
+    import torch
+    from factormodeling_amd import pipeline as PL
+    import factormodeling_amd.engine as E
+    D, A, F = 80, 130, 6
+    cfg = PL.workload_config("c5")
+    cfg.sel_window, cfg.factor_chunk, cfg.ret_ops = 20, 4, [("corr_vol", 15)]
+    cfg.select = cfg.composite = False
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=4, halo=cfg.halo)
+
+    class TwoPass(PL.EngineBackend):
+        corr_feature_max_w = 10
+
+    PL.run_ret_ops(sp, cfg, be=TwoPass())
+    two = sp.feature.clone()
+    sp.feature = None
+    PL.run_ret_ops(sp, cfg)
+    torch.cuda.synchronize()
+    assert np.array_equal(two.cpu().numpy(), sp.feature.cpu().numpy(), equal_nan=True)
+    assert 15 <= E.CORR_FEATURE_MAX_W

@@ -12,6 +12,11 @@ at, and sampled outputs are checked against the oracle / plain fp64 recomputatio
   rows, 64 sampled entries + their pair counts vs plain fp64 / integer recomputation.
 * C5 (2520 x 10000 x 500): 2 sampled factors' feature panel sign(ts_corr) * x / ts_std
   bit-exact vs the oracle, and their daily IC on sampled dates.
+* Discrete outputs vs the oracle alone: the icir_top selections of 3
+  (C2) / 2 (C5) consecutive processed days from ALL factors' window metrics recomputed by
+  the oracle (daily_stats on a host process pool, summarize, icir_top), C5's weighted
+  composite on 3 sampled days, C2's C entries among every kept pair, 256+ sampled C4
+  entries including the pairs among the first 16 kept factors.
 
 Each test frees its device memory before the next (C5 alone uses ~250 GB of HBM).
 """
@@ -64,6 +69,27 @@ def _greedy(C, order, rho, top):
             if top is not None and len(kept) >= top:
                 break
     return kept
+
+
+def _check_days_vs_oracle(P, R, cfg, proc, wn, win, rng, ndays, what):
+    """``ndays`` consecutive processed days: every factor's lag-L daily statistics over the
+    days' windows by the oracle (tests/oracle_pool.py: oracle.metrics.daily_stats of the
+    panel P's rows on a process pool), summarized per window; the step's weights wn[j] must
+    equal the oracle's icir_top selection bit for bit, and the step's window metrics win[j]
+    the oracle's to 1e-9."""
+    import oracle_pool
+    W, L = cfg.sel_window, cfg.ic_lags[-1]
+    j0 = int(rng.integers(0, len(proc) - ndays))
+    t_lo, t_hi = int(proc[j0]) - W + 1, int(proc[j0 + ndays - 1])
+    T = np.arange(t_lo, t_hi)
+    Xs = P[:, T - L].cpu().numpy()                              # exposures of target dates T
+    od = oracle_pool.daily_many(Xs, R[T])                       # [F][len(T)][4]
+    del Xs
+    for j in range(j0, j0 + ndays):
+        vals, wf = oracle_pool.window_selection(od, t_lo, int(proc[j]), W, cfg.icir_threshold, cfg.top_x)
+        assert_close(win[j][:, [0, 1, 2, 3, 4, 6]].ravel(), vals[:, [0, 1, 2, 3, 4, 6]].ravel(), rtol=1e-9,
+                     atol=1e-12, what=f"{what} window metrics, all factors, day {proc[j]}")
+        assert wf.sum() > 0 and np.array_equal(wf, wn[j]), f"{what} selection day {proc[j]} vs the oracle"
 
 
 def _prune_order(summ):
@@ -130,9 +156,15 @@ def test_c2_full_step_sampled_vs_oracle(dev):
         wf = np.zeros(F)
         wf[order] = wo
         assert np.array_equal(wf, wn[j]), f"selection day {i}"
-    # correlation Gram: 64 sampled entries vs plain fp64; kept = host greedy walk of C
+    # three consecutive processed days selected from ALL factors' window
+    # metrics recomputed by the oracle alone (daily_stats of the raw panel rows, summarize,
+    # icir_top), bit-for-bit equal to the step's weights
+    _check_days_vs_oracle(sp.X, R, cfg, proc, wn, win, rng, ndays=3, what="C2")
+    # correlation Gram: 64 sampled entries vs plain fp64, every pair among the kept factors
+    # too; kept = host greedy walk of C
     C = col["C"].cpu().numpy()
     pairs = [(int(a), int(b)) for a, b in rng.integers(0, F, size=(64, 2))]
+    pairs += [(a, b) for x, a in enumerate(kept) for b in kept[x + 1:]]
     for a, b in pairs:
         g, n = _zgram(sp.X[a], sp.X[b])
         assert n > 0
@@ -159,8 +191,9 @@ def test_c4_full_wide_gram(dev):
     assert float((d - 1.0).abs().max()) <= 1e-12
     rng = np.random.default_rng(4)
     Cn = C.cpu().numpy()
-    pairs = [(int(a), int(b)) for a, b in rng.integers(0, F, size=(64, 2))]
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, F, size=(256, 2))]
     pairs += [(0, F - 1), (F - 1, F - 1), (255, 256), (1023, 1024)]     # tile / block edges
+    pairs += [(a, b) for x, a in enumerate(kept[:16]) for b in kept[x + 1:16]]   # the first kept
     for a, b in pairs:
         g, n = _zgram(sp.X[a], sp.X[b])
         np.testing.assert_allclose(Cn[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
@@ -197,4 +230,21 @@ def test_c5_full_feature_sampled_vs_oracle(dev):
                 assert_close(daily[li, 1:, f, t], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12,
                              what=f"C5 IC L{L} f{f} t{t}")
     assert w.shape == (D - cfg.sel_window - 1, F)
+    # two consecutive days' selections from all 500 factors of the
+    # feature panel by the oracle, and the weighted composite of 3 sampled days
+    W = cfg.sel_window
+    proc = np.arange(W, D - 1)
+    wn = w.cpu().numpy()
+    win = col["win"].cpu().numpy()
+    _check_days_vs_oracle(sp.feature, R, cfg, proc, wn, win, rng, ndays=2, what="C5")
+    import oracle.composite as OC
+    comp = col["comp"]
+    names = cfg.names or PL.factor_names(F)
+    for j in sorted(rng.choice(len(proc), 3, replace=False)):
+        d = int(proc[j])
+        got = comp[d].cpu().numpy()
+        exp = OC.weighted_composite_factor(sp.feature[:, d:d + 1].cpu().numpy(), names, [0], wn[j:j + 1],
+                                           cfg.composite)[0]
+        assert np.abs(got).sum() > 0
+        assert_close(got, exp, rtol=1e-6, atol=1e-9, what=f"C5 weighted composite day {d}")
     del sp, col, w

@@ -172,3 +172,20 @@ def test_ts_corr_window60_vs_pandas():
     y, _ = dense(st, "in_y", D, A)
     out = O.ts_corr(x, y, 60, present=p)
     assert_close(gather(out, st, "out_ts_corr_60"), st["out_ts_corr_60__v"], exact=True, what="ts_corr_60")
+
+
+def test_pairwise_sum_is_numpys_sum():
+    """oracle.numerics.pairwise_sum restates numpy's float64 add.reduce (128-element leaves
+    with 8 accumulators, splits at multiples of 8, 8192-element buffer chunks) bit for bit:
+    pinned here against numpy itself at lengths around every boundary, which is what lets
+    the full-size checks' process pools (tests/oracle_pool.py) use numpy's sum directly."""
+    import oracle.numerics as nm
+    rng = np.random.default_rng(12)
+    lens = sorted({1, 7, 8, 9, 127, 128, 129, 255, 256, 257, 1000, 4999, 5000, 8191, 8192, 8193,
+                   10000, 16384, 16385, 20000} | set(rng.integers(1, 30000, 40).tolist()))
+    assert not nm.FAST
+    for n in lens:
+        a = rng.standard_normal(n) * np.exp(rng.uniform(-30, 30, n))
+        assert nm.pairwise_sum(a) == np.add.reduce(a), n
+        b = a.reshape(1, -1)
+        assert nm.pairwise_sum(b)[0] == np.add.reduce(a), n

@@ -64,3 +64,16 @@ def test_mvo_selector_needs_the_reference_checkout(monkeypatch):
     df = pd.DataFrame({"IC_IR": [0.1], "rank_IC_IR": [0.1]}, index=["a"])
     with pytest.raises(NotImplementedError, match="FMX_REFERENCE_DIR"):
         M.mvo_selector(df, None, None, pd.DataFrame({"a": [0.01]}), "t", 1)
+
+
+def test_ledoit_wolf_shrinkage_matches_reference_golden():
+    """factor_selection_methods.py:60-117 vs vectors the reference itself produced
+    (tests/golden/make_golden_lw.py): generic, a constant factor (excluded from the mean
+    correlation), more factors than observations -- bit for bit."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "ledoit_wolf.npz"))
+    for name in ("generic", "const", "wide"):
+        got = M.ledoit_wolf_shrinkage(g[f"{name}_in"])
+        assert np.array_equal(got, g[f"{name}_out"]), name
+    with pytest.raises(ValueError):                  # one factor: np.diag of a 0-d cov (as the reference)
+        M.ledoit_wolf_shrinkage(np.zeros((10, 1)))

@@ -1,4 +1,4 @@
-"""Date-sharded multi-rank step on CPU (gloo, world_size 2 and 3) vs a single-rank run.
+"""Date-sharded multi-rank step on CPU (gloo, world_size 2, 3 and 4) vs a single-rank run.
 
 The product's distributed logic (factormodeling_amd.pipeline: halo exchange by
 send/recv, IC all-gather, Gram all-reduce, redundant selection) runs unchanged; the
@@ -69,9 +69,10 @@ def _launch(world, skip_halo=False):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_step_matches_single_rank(world):
-    """2 ranks: one boundary; 3 ranks: a middle rank both receives and sends its halo."""
+    """2 ranks: one boundary; 3 ranks: a middle rank both receives and sends its halo;
+    4 ranks: two middle ranks (the halo slabs travel as one batch_isend_irecv group)."""
     from factormodeling_amd import pipeline as PL
     res = _launch(world)
     # single-rank reference (no process group needed for world == 1)
@@ -123,6 +124,14 @@ def test_shard_bounds_cover_dates():
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
         assert all(lo % B == 0 for lo, _ in spans)
         PL.check_sharding(2520, world, 61, B)
+    # short panels split whole blocks evenly -- 200 dates = 13 blocks of 16 over 8
+    # ranks leave no rank empty (the old ceil(D / world) rounding gave rank 7 [200, 200))
+    for D, world in ((200, 8), (100, 4), (33, 3), (2520, 7)):
+        spans = [PL.shard_bounds(D, world, r, B) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == D
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+        assert all(hi > lo for lo, hi in spans) and all(lo % B == 0 for lo, _ in spans)
+        PL.check_sharding(D, world, 1, B)
 
 
 def test_rank_owning_fewer_dates_than_halo_is_rejected():
