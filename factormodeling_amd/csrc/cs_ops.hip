@@ -84,7 +84,7 @@ k_cs_moment(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int
             double* __restrict__ Y2) {
   extern __shared__ double lds[];
   __shared__ int32_t sch_l[PW_LDS_MAX];              // dense rows: the schedule for n = A
-  const int64_t row = blockIdx.x;
+  const int64_t row = fmx_blk();                     // grid dim3(D, F)
   const int64_t d = row % D;
   const double* x = X + row * ld;
   double* y = Y ? Y + row * ld : nullptr;
@@ -797,7 +797,7 @@ static fmx_status cs_moment_launch(int op, const double* X, double* Y, int64_t F
   }
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&present, (void*)&pw, (void*)&stats,
                   (void*)&slen, (void*)&Y2};
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(CSM_NT), args, lds, as_stream(stream)));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(CSM_NT), args, lds, as_stream(stream)));
   return FMX_OK;
 }
 

@@ -494,105 +494,81 @@ __device__ void fr_scan16(uint32_t* w, int* scr) {
 // ---- List-balanced in-bucket scans ---------------------------------------------------
 // An element sharing a fine bucket with other, distinct keys needs #less / #equal among the
 // bucket's n members.  Scanned by its owning lane (one exec-masked loop per element slot),
-// a wave pays max-over-lanes(n) iterations per slot while only ~40 % of its lanes have work
-// (C5's ranks-only pass spent 42 % of its time there).  Instead every such element becomes
-// a 32-bit work item (bucket start | slot << 16 | n << 24) in an LDS list that all threads
-// walk, and the result (#less | #equal << 16) replaces the item.  Two kinds of item:
-// pairs (n = 2: one compare with the other member, no loop) fill the list from the front,
-// larger buckets (n <= 255) from the back, so consecutive items have similar work.  Index
-// claims are ballot prefix counts per wave (no atomics); items past the list's capacity or
-// with n > 255 are scanned by their owner (FR_SELF).
+// a wave pays max-over-lanes(n) iterations per slot while only ~40 % of its lanes have work.
+// Instead every such element becomes a 32-bit work item (bucket start | slot << 16 | n << 24)
+// in its WAVE's region of an LDS list; the wave walks its region with all lanes busy and the
+// result (#less | #equal << 16) replaces the item.  Two kinds of item: pairs (n = 2: one
+// compare with the other member, no loop) fill the region from the front, larger buckets
+// (n <= 255) from the back, so consecutive items have similar work.  Claims are ballot
+// prefix counts (no atomics, no cross-wave bases), the items are written while the counters
+// are read, and the wave that claimed an item reads its result: no barrier of its own.
+// Items that do not fit the region or have n > 255 are scanned by their owner (FR_SELF).
 constexpr int FR_SELF = (int)0x80000000u;
 
 struct FrClaim {
   int a = 0, b = 0;          // the wave's pair / multi items so far (wave-uniform)
 };
-// ref: slot | kind << 8 | index-in-wave << 10 (kind 0 pair, 1 multi), or slot | FR_SELF.
-__device__ __forceinline__ int fr_claim(FrClaim& c, bool scan, int n, int slot) {
+// Claim (and write) the work item of one element slot across the wave.  items: the wave's
+// region of wcap items.  Returns the item index | slot << 14, or slot | FR_SELF.  A slot's
+// claims are all taken or all refused (region full), so the front and back never meet.
+__device__ __forceinline__ int fr_claim_put(FrClaim& c, uint32_t* items, int wcap, bool scan, int n, int slot,
+                                            int s0) {
   const bool pa = scan && n == 2, pb = scan && (unsigned)(n - 3) <= 252u;
   const uint64_t ma = __builtin_amdgcn_ballot_w64(pa), mb = __builtin_amdgcn_ballot_w64(pb);
+  const int na = __popcll(ma), nb = __popcll(mb);
+  const bool fits = c.a + na + c.b + nb <= wcap;        // wave-uniform
   // (a select of the whole mask and a ternary ref: the branch-free forms of both made the
   // compiler spill in the 80- and 128-VGPR rank kernels)
   const uint64_t m = pa ? ma : mb;
   const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  const int idx = (pa ? c.a : c.b) + below;
-  c.a += __popcll(ma);
-  c.b += __popcll(mb);
-  return pa ? (slot | idx << 10) : (pb ? (slot | 1 << 8 | idx << 10) : (slot | FR_SELF));
-}
-// After every slot's claim: lane 0 parks the wave's totals (wtot: NT/64 entries).
-__device__ __forceinline__ void fr_claim_publish(int2* wtot, const FrClaim& c) {
-  if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = make_int2(c.a, c.b);
-}
-// After a barrier: the wave's bases and the list's occupancy (pairs [0, na), multis
-// [cap - nb, cap)).
-struct FrListBase {
-  int a0, b0, na, nb, cap;
-  template <int NW>
-  __device__ __forceinline__ static FrListBase make(const int2* wtot, int cap_) {
-    FrListBase r;
-    r.init<NW>(wtot, cap_);
-    return r;
+  const int g = pa ? c.a + below : wcap - 1 - (c.b + below);
+  if (fits) {
+    c.a += na;
+    c.b += nb;
   }
-  template <int NW>
-  __device__ __forceinline__ void init(const int2* wtot, int cap_) {
-    const int wid = threadIdx.x >> 6;
-    int ta = 0, tb = 0;
-    a0 = b0 = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const int2 v = wtot[w];
-      a0 += w < wid ? v.x : 0;
-      b0 += w < wid ? v.y : 0;
-      ta += v.x;
-      tb += v.y;
-    }
-    cap = cap_;
-    na = ta < cap ? ta : cap;
-    nb = tb < cap - na ? tb : cap - na;
-  }
-};
-// Scatter of a scanned element: its key into the bucket range, its work item into the
-// list.  Returns the list index, or slot | FR_SELF when its owner scans it.
-__device__ __forceinline__ int fr_list_put(uint64_t* bkey, uint32_t* items, const FrListBase& lb, int ref, int s0,
-                                           int n, uint64_t key) {
-  const bool self = ref < 0;
-  const int slot = self ? (ref & 0x3fff) : (ref & 0xff);
-  bkey[s0 + slot] = key;
-  if (self) return ref;
-  const int idx = ref >> 10;
-  const bool multi = (ref >> 8) & 1;
-  const int g = multi ? lb.cap - 1 - (lb.b0 + idx) : lb.a0 + idx;
-  const bool ok = multi ? g >= lb.cap - lb.nb : g < lb.na;
-  if (!ok) return slot | FR_SELF;
-  items[g] = (uint32_t)s0 | ((uint32_t)slot << 16) | ((uint32_t)n << 24);
-  return g;
+  const bool take = fits && (pa || pb);
+  if (take) items[g] = (uint32_t)s0 | ((uint32_t)slot << 16) | ((uint32_t)n << 24);
+  return take ? (g | slot << 14) : (slot | FR_SELF);
 }
-// Every thread: walk the list, result #less | #equal << 16 in place of each item.
-template <int NT>
-__device__ __forceinline__ void fr_list_walk(const uint64_t* bkey, uint32_t* items, const FrListBase& lb) {
-  for (int g = threadIdx.x; g < lb.na; g += NT) {            // pairs: one compare
+// The wave walks its own region: pairs [0, a), multis [wcap - b, wcap); result
+// #less | #equal << 16 in place of each item, visible to the whole wave on return.
+__device__ __forceinline__ void fr_list_walk_wave(const uint64_t* bkey, uint32_t* items, int wcap, const FrClaim& c) {
+  const int lane = fr_lane();
+  for (int g = lane; g < c.a; g += 64) {                // pairs: one compare
     const uint32_t it = items[g];
     const uint64_t* bk = bkey + (it & 0xffffu);
     const int slot = (int)((it >> 16) & 1u);
     const uint64_t own = bk[slot], oth = bk[slot ^ 1];
     items[g] = (uint32_t)((oth < own ? 1 : 0) + (oth == own ? 0x20000 : 0x10000));
   }
-  for (int g = lb.cap - lb.nb + (int)threadIdx.x; g < lb.cap; g += NT) {
+  for (int g = wcap - c.b + lane; g < wcap; g += 64) {  // two members per step: two reads in flight
     const uint32_t it = items[g];
     const uint64_t* bk = bkey + (it & 0xffffu);
     const int slot = (int)((it >> 16) & 0xffu), n = (int)(it >> 24);
     const uint64_t own = bk[slot];
     int acc = 0;
-    for (int j = 0; j < n; ++j) {
-      const uint64_t w = bk[j];
-      acc += (w < own ? 1 : 0) + (w == own ? 0x10000 : 0);
+    for (int j = 0; j < n; j += 2) {
+      const int j1 = j + 1 < n ? j + 1 : j;
+      const uint64_t w0 = bk[j], w1 = bk[j1];
+      acc += (w0 < own ? 1 : 0) + (w0 == own ? 0x10000 : 0);
+      acc += j + 1 < n ? (w1 < own ? 1 : 0) + (w1 == own ? 0x10000 : 0) : 0;
     }
     items[g] = (uint32_t)acc;
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// Owner scan of an element the list did not take: #less | #equal << 16.
-__device__ __forceinline__ int fr_self_scan(const uint64_t* bk, int n, uint64_t own) {
+// Scatter of a scanned element's key into its bucket range (after the counters are dead).
+__device__ __forceinline__ void fr_scatter_key(uint64_t* bkey, int ref, int s0, uint64_t key) {
+  const int slot = ref < 0 ? (ref & 0x3fff) : ((ref >> 14) & 0xff);
+  bkey[s0 + slot] = key;
+}
+// Result of a scanned element: its item's, or its own scan when the list did not take it.
+__device__ __forceinline__ int fr_result(const uint64_t* bkey, const uint32_t* items, int ref, int s0, int n) {
+  if (ref >= 0) return (int)items[ref & 0x3fff];
+  const uint64_t* bk = bkey + s0;
+  const uint64_t own = bk[ref & 0x3fff];
   int acc = 0;
   for (int j = 0; j < n; ++j) {
     const uint64_t w = bk[j];

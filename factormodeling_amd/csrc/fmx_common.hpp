@@ -71,6 +71,13 @@ __device__ __forceinline__ double mdiv(double x, double n, double r) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Row kernels launch their F * D (or D * F) rows as a 2-D grid dim3(inner, outer) and read
+// the row as fmx_blk(): the work-items of ONE grid dimension are a 32-bit count, so a 1-D
+// grid of rows x 1024 threads wraps past 4.19M rows (C4's 5.04M daily-IC rows ran only the
+// first 846,000 -- the rest of the output was never written).
+__device__ __forceinline__ int64_t fmx_blk() { return (int64_t)blockIdx.y * gridDim.x + blockIdx.x; }
+inline dim3 fmx_grid2(int64_t inner, int64_t outer) { return dim3((unsigned)inner, (unsigned)outer); }
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace fmx

@@ -22,7 +22,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   if (rank_impl() == RANK_IMPL_BR || !lds_fits(kfr, lds_fr)) {
     void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present};
     const size_t lds = (size_t)std::max<int64_t>(A, nt) * 8;
-    return launch_br(FMX_EMAX_TABLE(k_cs_rank_br), nt, A, F * D, lds, args, st);
+    return launch_br(FMX_EMAX_TABLE(k_cs_rank_br), nt, A, D, F, lds, args, st);
   }
   double* Y2 = nullptr;
   double qlo = 0.0, qhi = 0.0;
@@ -36,7 +36,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(kfr, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(kfr, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -60,7 +60,7 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -87,7 +87,7 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -131,7 +131,7 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 

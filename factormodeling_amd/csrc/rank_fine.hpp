@@ -96,8 +96,8 @@ struct FrIcRow {
 
 __device__ __forceinline__ FrIcRow fr_ic_row(const FrIc& ic, int64_t D) {
   FrIcRow r;
-  r.s = (int64_t)blockIdx.x / ic.F;
-  r.f = (int64_t)blockIdx.x % ic.F;
+  r.s = fmx_blk() / ic.F;                     // grid dim3(F, D): date-major rows
+  r.f = fmx_blk() % ic.F;
   r.lag[0] = ic.L0;
   r.lag[1] = ic.L1;
 #pragma unroll
@@ -183,7 +183,7 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
       if (fr_in<NT>(t, k, (int)A)) ic.RK[row * ld + t + k * NT] = (fmx_rank2_t)fr_r2<EMAX>(r2, k);
     if (t == 0) {
       const int q = atomicAdd(&ic.ovf[0], 1);
-      ic.ovf[1 + q] = (int32_t)blockIdx.x;
+      ic.ovf[1 + q] = (int32_t)fmx_blk();
     }
     return;
   }
@@ -375,7 +375,6 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   __shared__ FrTab tab;
   __shared__ uint4 wred[NW];                  // per wave: #present, #valid, min / max key high words
   __shared__ int iscr[NW];
-  __shared__ int2 lwt[NW];                    // in-bucket scan list: per-wave claim totals
   // dynamic: max(A keys, WORDS packed counters), then the scan list (lcap items; with ZN the
   // moments' schedule and tree nodes alias it)
   extern __shared__ uint64_t lds[];
@@ -395,7 +394,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     rw = fr_ic_row(ic, D);
     if (t < 2) ic_ne[t] = 0;
   }
-  const int64_t row = IC ? rw.f * D + rw.s : (int64_t)blockIdx.x;
+  const int64_t row = IC ? rw.f * D + rw.s : fmx_blk();   // grid dim3(D, F)
   const double* x = X + row * ld;
   double* y = Y + row * ld;
   const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
@@ -542,45 +541,39 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   fr_scan16<NT, WORDS>(cnt, iscr);
   BR_PH();
   // le[k] = #less | #equal << 16 inside the bucket; for elements still to scan (n field of
-  // sl set) first their list claim (fr_list_claim), then their list index or slot | FR_SELF
+  // sl set) first their work item in the wave's list region (fr_claim_put)
   int le[EMAX];
-  FrClaim lcl;
-#pragma unroll
-  for (int k = 0; k < EMAX; ++k) {
-    const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
-    const int slot = sl[k] & PK_SLOT;
-    int s0, s1;
-    fr_cnt_get2(cnt, b, &s0, &s1);
-    const int n = s1 - s0;
-    const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
-    const bool scan = !eqb && n > 1 && b != DUMMY;
-    const int ref = fr_claim(lcl, scan, n, slot);
-    le[k] = scan ? ref : (eqb ? n : 1) << 16;
-    sl[k] = s0 | (scan ? n << 16 : 0);
-    FR_SCHED_FENCE();
-  }
-  fr_claim_publish(lwt, lcl);
-  __syncthreads();                            // counters dead: the keys reuse their LDS
   {
-    const FrListBase lb = FrListBase::make<NW>(lwt, lcap);
+    const int wcap = lcap / NW;
+    uint32_t* witems = litems + wid * wcap;
+    FrClaim lcl;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
-      const int n = sl[k] >> 16;
-      if (n) le[k] = fr_list_put(bkey, litems, lb, le[k], sl[k] & 0xffff, n, key[k]);
+      const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
+      const int slot = sl[k] & PK_SLOT;
+      int s0, s1;
+      fr_cnt_get2(cnt, b, &s0, &s1);
+      const int n = s1 - s0;
+      const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
+      const bool scan = !eqb && n > 1 && b != DUMMY;
+      const int ref = fr_claim_put(lcl, witems, wcap, scan, n, slot, s0);
+      le[k] = scan ? ref : (eqb ? n : 1) << 16;
+      sl[k] = s0 | (scan ? n << 16 : 0);
+      FR_SCHED_FENCE();
     }
+    __syncthreads();                          // counters dead: the keys reuse their LDS
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (sl[k] >> 16) fr_scatter_key(bkey, le[k], sl[k] & 0xffff, key[k]);
     __syncthreads();
     BR_PH();
 #ifndef FR_DIAG_NOSCAN
-    fr_list_walk<NT>(bkey, litems, lb);
+    fr_list_walk_wave(bkey, witems, wcap, lcl);
 #endif
-    __syncthreads();
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       const int n = sl[k] >> 16;
-      if (n) {
-        const uint64_t* bk = bkey + (sl[k] & 0xffff);
-        le[k] = le[k] >= 0 ? (int)litems[le[k]] : fr_self_scan(bk, n, bk[le[k] & 0x3fff]);
-      }
+      if (n) le[k] = fr_result(bkey, witems, le[k], sl[k] & 0xffff, n);
     }
   }
   const double den = (double)(nrow - 1);
@@ -721,7 +714,6 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
   __shared__ FrTab tab;
   __shared__ uint4 wred[NW];
   __shared__ int iscr[NW];
-  __shared__ int2 lwt[NW];
   extern __shared__ uint64_t lds[];           // max(A keys, WORDS packed counters), then the scan list
   uint32_t* cnt = (uint32_t*)lds;
   uint64_t* bkey = lds;
@@ -796,8 +788,10 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
     BR_PH();
     fr_scan16<NT, WORDS>(cnt, iscr);
     BR_PH();
-    int le[EMAX];                             // list claim / index, then c = 2 #less + #equal in the bucket
+    int le[EMAX];                             // work item / slot, then c = 2 #less + #equal in the bucket
     uint32_t nan_m = 0;
+    const int wcap = lcap / NW;
+    uint32_t* witems = litems + wid * wcap;
     FrClaim lcl;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
@@ -809,33 +803,27 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
       const bool scan = !eqb && n > 1 && b != DUMMY;
       nan_m |= (uint32_t)(b == DUMMY) << k;
-      const int ref = fr_claim(lcl, scan, n, slot);
+      const int ref = fr_claim_put(lcl, witems, wcap, scan, n, slot, s0);
       le[k] = scan ? ref : (eqb ? n : 1);
       sl[k] = s0 | (scan ? n << 16 : 0);
       FR_SCHED_FENCE();
     }
-    fr_claim_publish(lwt, lcl);
     __syncthreads();                          // counters dead: the keys reuse their LDS
     BR_PH();
-    const FrListBase lb = FrListBase::make<NW>(lwt, lcap);
 #pragma unroll
-    for (int k = 0; k < EMAX; ++k) {
-      const int n = sl[k] >> 16;
-      if (n) le[k] = fr_list_put(bkey, litems, lb, le[k], sl[k] & 0xffff, n, key[k]);
-    }
+    for (int k = 0; k < EMAX; ++k)
+      if (sl[k] >> 16) fr_scatter_key(bkey, le[k], sl[k] & 0xffff, key[k]);
     __syncthreads();
     BR_PH();
 #ifndef FR_DIAG_NOSCAN
-    fr_list_walk<NT>(bkey, litems, lb);
+    fr_list_walk_wave(bkey, witems, wcap, lcl);
 #endif
-    __syncthreads();
     BR_PH();
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       const int n = sl[k] >> 16;
       if (n) {
-        const uint64_t* bk = bkey + (sl[k] & 0xffff);
-        const int c = le[k] >= 0 ? (int)litems[le[k]] : fr_self_scan(bk, n, bk[le[k] & 0x3fff]);
+        const int c = fr_result(bkey, witems, le[k], sl[k] & 0xffff, n);
         le[k] = 2 * (c & 0xffff) + (c >> 16);
       }
     }
@@ -879,7 +867,7 @@ k_cs_quantile_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D
   uint32_t* cnt = (uint32_t*)lds;
   uint64_t* lists = lds;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int64_t row = blockIdx.x;
+  const int64_t row = fmx_blk();              // grid dim3(D, F)
   const double* x = X + row * ld;
   double* y = Y + row * ld;
   const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;
@@ -1103,7 +1091,7 @@ k_ic_daily_fr(const double* __restrict__ X, const double* __restrict__ Rt, int64
   BR_PH_INIT;
   // date-major rows: the F workgroups of a date share its return rows in L2 (measured
   // faster than factor-major order at C2: 44.8 vs 46.5 ms)
-  const int64_t s = blockIdx.x / F, f = blockIdx.x % F;
+  const int64_t s = fmx_blk() / F, f = fmx_blk() % F;   // grid dim3(F, D)
   const double* xf = X + (f * D + s) * ld;
   const int lagv[2] = {L0, L1};
   const double* rr[2];

@@ -42,8 +42,9 @@ fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, i
     FMX_LAUNCH_CHECK("k_ic_empty");
     void* args[] = {(void*)&X, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0, (void*)&L1,
                     (void*)&NL, (void*)&o};
-    fmx_status e = fine ? launch_br(fr_table, nt, A, F * D, lds, args, st)
-                        : launch_br(FMX_EMAX_TABLE(k_ic_daily_br), nt, A, F * D, lds, args, st);
+    // date-major rows (s = row / F): grid dim3(F, D)
+    fmx_status e = fine ? launch_br(fr_table, nt, A, F, D, lds, args, st)
+                        : launch_br(FMX_EMAX_TABLE(k_ic_daily_br), nt, A, F, D, lds, args, st);
     if (e) return e;
   }
   return FMX_OK;
@@ -479,7 +480,7 @@ fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const d
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(F, D), dim3(nt_fa), args, ll.bytes, st));   // date-major rows
   static const int list_grid = [] {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -78,7 +78,7 @@ k_cs_rank_br(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   extern __shared__ uint64_t bkey[];          // max(A, NT) keys
   const int t = threadIdx.x;
   BR_PH_INIT;
-  const int64_t row = blockIdx.x;
+  const int64_t row = fmx_blk();              // grid dim3(D, F)
   const int64_t d = row % D;
   const double* x = X + row * ld;
   double* y = Y + row * ld;
@@ -201,7 +201,7 @@ k_cs_quantile_br(const double* __restrict__ X, double* __restrict__ Y, int64_t D
   extern __shared__ uint64_t lists[];         // 4 * QCAP keys (also splitter scratch)
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   BR_PH_INIT;
-  const int64_t row = blockIdx.x;
+  const int64_t row = fmx_blk();              // grid dim3(D, F)
   const int64_t d = row % D;
   const double* x = X + row * ld;
   double* y = Y + row * ld;
@@ -355,7 +355,7 @@ k_ic_daily_br(const double* __restrict__ X, const double* __restrict__ Rt, int64
   uint8_t* bmask = (uint8_t*)(bkey + kcap);
   const int t = threadIdx.x;
   BR_PH_INIT;
-  const int64_t s = blockIdx.x / F, f = blockIdx.x % F;
+  const int64_t s = fmx_blk() / F, f = fmx_blk() % F;   // grid dim3(F, D)
   const double* xf = X + (f * D + s) * ld;
   const int lagv[2] = {L0, L1};
   const double* rr[2];

@@ -74,15 +74,16 @@ static inline FrListLds fr_list_lds(const void* k, int64_t A, size_t base, size_
   return r;
 }
 
+// rows = inner * outer blocks on a 2-D grid (fmx_grid2; the kernel reads its row as fmx_blk())
 template <class K>
-static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t nblocks, size_t lds, void** args,
-                                   hipStream_t st) {
+static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t inner, int64_t outer, size_t lds,
+                                   void** args, hipStream_t st) {
   const void* k = kern_table(nt, br_emax(A, nt));
   if (!k) { set_error("row too long for the bucket-rank kernels (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
-  if (nblocks <= 0) return FMX_OK;
-  if (nblocks > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
+  if (inner <= 0 || outer <= 0) return FMX_OK;
+  if (inner * nt > 0xffffffffll || outer > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  FMX_HIP(hipLaunchKernel(k, dim3((unsigned)nblocks), dim3(nt), args, lds, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(inner, outer), dim3(nt), args, lds, st));
   return FMX_OK;
 }
 

@@ -26,14 +26,14 @@ fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t
     if (k && lds_fits(k, lds_f)) {
       if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
       if (F * D == 0) return FMX_OK;
-      FMX_HIP(hipLaunchKernel(k, dim3((unsigned)(F * D)), dim3(ntf), args, lds_f, st));
+      FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(ntf), args, lds_f, st));
       return FMX_OK;
     }
   }
   const int nt = br_nt(512);
   const size_t lds = (size_t)4 * QCAP * 8;
-  if (op == 0) return launch_br(FMX_EMAX_TABLE(kq0), nt, A, F * D, lds, args, st);
-  return launch_br(FMX_EMAX_TABLE(kq1), nt, A, F * D, lds, args, st);
+  if (op == 0) return launch_br(FMX_EMAX_TABLE(kq0), nt, A, D, F, lds, args, st);
+  return launch_br(FMX_EMAX_TABLE(kq1), nt, A, D, F, lds, args, st);
 }
 
 }  // namespace fmx

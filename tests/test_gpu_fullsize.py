@@ -198,7 +198,18 @@ def test_c4_full_wide_gram(dev):
         g, n = _zgram(sp.X[a], sp.X[b])
         np.testing.assert_allclose(Cn[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
     assert kept == _greedy(Cn, _prune_order(col["summ"].cpu().numpy()), cfg.prune_rho, None)
-    del sp, col, C
+    # the daily IC the pruning order comes from, on sampled (factor, date) pairs across the
+    # whole panel (rows past 4.19M of a 1-D grid of 1024-thread rows once went unwritten)
+    daily = col["daily"]
+    R = sp.R.cpu().numpy()
+    L = cfg.ic_lags[0]
+    for f, t in zip(rng.integers(0, F, 24), rng.integers(L, D, 24)):
+        f, t = int(f), int(t)
+        n, ic, ric, beta = OM.daily_stats(sp.X[f, t - L].cpu().numpy(), R[t])
+        got = daily[0, :, f, t].cpu().numpy()
+        assert got[0] == n, (f, t)
+        assert_close(got[1:], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12, what=f"C4 IC f{f} t{t}")
+    del sp, col, C, daily
 
 
 @pytest.mark.timeout(900)

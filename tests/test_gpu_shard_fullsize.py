@@ -51,7 +51,7 @@ def _run(dev, world, D, A, F, cfg, fs):
         w, kept = PL.run_step(sp, cfg, collect=col)
         torch.cuda.current_stream().synchronize()
         out = (sp.d_lo, sp.d_hi, None if w is None else w.cpu().numpy(), kept, col["C"].cpu().numpy(),
-               _host(col, keys))
+               _host(col, keys), col["daily"].cpu().numpy(), col["summ"].cpu().numpy())
         del sp, col, w
         return out
 
@@ -61,12 +61,15 @@ def _run(dev, world, D, A, F, cfg, fs):
 
 
 def _compare(res1, res, cfg):
-    (_, _, w1, kept1, C1, ops1), = res1
-    for lo, hi, w, kept, C, ops in res:
+    (_, _, w1, kept1, C1, ops1, daily1, summ1), = res1
+    for lo, hi, w, kept, C, ops, daily, summ in res:
+        assert np.array_equal(C, C1), lo                            # exact Gram: same bits
+        bad = np.argwhere(~((daily == daily1) | (np.isnan(daily) & np.isnan(daily1))))
+        assert bad.size == 0, (lo, len(bad), bad[:8].tolist())      # gathered daily IC series
+        assert np.array_equal(summ, summ1, equal_nan=True), lo      # full-sample metrics
         if w1 is not None:
             assert np.array_equal(w, w1), lo                        # selections
         assert kept == kept1, lo                                    # pruned set
-        assert np.array_equal(C, C1), lo                            # exact Gram: same bits
         for k, v in ops.items():
             ref = ops1[k][:, lo:hi]
             if k.startswith("ts:"):
