@@ -27,6 +27,7 @@
 namespace fmx {
 
 constexpr int FR_S = 64;   // samples = one wave
+constexpr int FR_BEQ = 1 << 16;   // bucket-id flag of an equal-to-sample bucket (EQB searches)
 
 // Lane index re-read at every call site: the persistent kernels loop over rows, and
 // without this the compiler hoists every shuffle's lane-derived address (and the bitonic
@@ -358,7 +359,6 @@ __device__ __forceinline__ void fr_park_sample(FrTab& T, const uint64_t* key) {
 }
 
 // EQB: an equal-to-sample bucket id also carries FR_BEQ (callers mask it off for the counter)
-constexpr int FR_BEQ = 1 << 16;
 template <int K, int G, bool EQB = false>
 __device__ __forceinline__ void fr_bucket_grp(const FrTab& T, const uint64_t* key, int* b, int dummy) {
   int i[G];
@@ -555,9 +555,10 @@ __device__ __forceinline__ void fr_list_walk_wave(const uint64_t* bkey, uint32_t
     }
     items[g] = (uint32_t)acc;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // the wave's own LDS writes complete before any lane reads them back: lgkmcnt only (a
+  // fence would also wait out vmcnt -- the persistent kernel's next-row loads in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // Scatter of a scanned element's key into its bucket range (after the counters are dead).
 __device__ __forceinline__ void fr_scatter_key(uint64_t* bkey, int ref, int s0, uint64_t key) {

@@ -64,77 +64,6 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   return FMX_OK;
 }
 
-// cs_rank + cs_winsor (+ doubled ranks) + cs_zscore + market_neutralize of dense rows in one
-// pass (k_cs_rank_fa<ZN>); FMX_ERR_UNSUPPORTED when the row does not fit the fine kernel.
-template <int NT, int E> constexpr auto kcrwz_dense = k_cs_rank_fa<NT, E, false, true, false, true>;
-fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double* Yz, double* Yn, int64_t F, int64_t D,
-                                int64_t A, int64_t ld, double qlo, double qhi, fmx_rank2_t* RK, PwTable pw, int slen,
-                                hipStream_t st) {
-  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
-  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
-  const int E = br_emax(A, nt_fa);
-  const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcrwz_dense)(nt_fa, E);
-  if (rank_impl() == RANK_IMPL_BR || !k || !lds_fits(k, lds_fr)) return FMX_ERR_UNSUPPORTED;
-  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
-  if (F * D == 0) return FMX_OK;
-  int method = FMX_RANK_AVERAGE;
-  const uint8_t* present = nullptr;
-  FrIc ic{};
-  FrZn zn{Yz, Yn, pw, slen};
-  // the moments' scratch sits where the scan list goes later
-  const FrListLds ll = fr_list_lds(k, A, (size_t)fr_list_off(A, FR_CS_WORDS), FR_ZN_SCR_BYTES);
-  int lcap = ll.cap;
-  void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
-  return FMX_OK;
-}
-
-// Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
-// raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
-// Rows of 8193..10240 assets (C5) take the persistent k_cs_rank2_pf (one row per CU, the
-// next row's loads in flight, no spills); FMX_RANK2_PF=0 keeps k_cs_rank_fa for A/B.
-static bool rank2_pf_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("FMX_RANK2_PF");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
-  const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
-  const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
-  const int E = br_emax(A, nt_fa);
-  if (nt_fa == 1024 && E == 10 && rank_impl() == RANK_IMPL_FINE && rank2_pf_enabled()) {
-    int64_t nrows = F * D;
-    const void* kp = (const void*)k_cs_rank2_pf<1024, 10>;
-    const FrListLds ll = fr_list_lds(kp, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
-    int lcap = ll.cap;
-    void* args[] = {(void*)&X, (void*)&nrows, (void*)&A, (void*)&ld, (void*)&RK, (void*)&lcap};
-    return launch_persistent(kp, 1024, nrows, ll.bytes, args, st);
-  }
-  const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense)(nt_fa, E);
-  if (!k || !lds_fits(k, lds_fr)) { set_error("fmx_cs_rank2: A <= 16384"); return FMX_ERR_UNSUPPORTED; }
-  if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
-  if (F * D == 0) return FMX_OK;
-  double* Y = nullptr;
-  double* Y2 = nullptr;
-  int method = FMX_RANK_AVERAGE;
-  const uint8_t* present = nullptr;
-  double qlo = 0.0, qhi = 0.0;
-  FrIc ic{};
-  FrZn zn{};
-  const FrListLds ll = fr_list_lds(k, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
-  int lcap = ll.cap;
-  void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
-                  (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
-  return FMX_OK;
-}
-
 }  // namespace fmx
 
 BR_PHASE_EXPORT(fmx_debug_phase_cs)

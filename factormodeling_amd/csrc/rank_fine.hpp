@@ -430,6 +430,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     if constexpr (ZN)
       if (in) reinterpret_cast<double*>(lds)[fr_opaque(t) + k * NT] = v;   // the row for the moments
   }
+  BR_PH();
   if constexpr (ZN) {
     // cs_zscore / market_neutralize: numpy nanmean and nanvar (ddof 0) by the pairwise
     // schedule of n = A (NaN -> 0 in the sums, counted apart), as k_cs_moment_rg
@@ -449,6 +450,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
                                           [&](int i) { return (int)(vrow[i] == vrow[i]); }, sch, zn_nodes,
                                           zn_iscr, &cnt);
     const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
+    BR_PH();
     const double s2 = block_pw_sum_w0<NT>([&](int i) {
       const double u = vrow[i];
       const double z = u == u ? u : 0.0;
@@ -457,6 +459,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     }, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
     const double var = cnt > 0 ? s2 / (double)cnt : qnan();
 #endif
+    BR_PH();
     const double sd = sqrt(var);
     const bool g2 = sd == 0.0 || sd != sd;     // neutralize: sigma in {0, NaN} -> 0
     double* yz = zn.Yz + row * ld;
@@ -470,6 +473,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       __builtin_nontemporal_store(g2 ? 0.0 : o, yn + ia);
     }
     __syncthreads();                          // every read of the staged row is done
+    BR_PH();
   }
   fr_park_sample<NT, EMAX>(tab, key);
 #pragma unroll
@@ -538,6 +542,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     for (int k = 0; k < EMAX; ++k) sl[k] = (int)fr_cnt_add(cnt, bb[k] & (FR_BEQ - 1)) | (bb[k] << PK_BSHIFT);
   }
   __syncthreads();
+  BR_PH();
   fr_scan16<NT, WORDS>(cnt, iscr);
   BR_PH();
   // le[k] = #less | #equal << 16 inside the bucket; for elements still to scan (n field of
@@ -562,6 +567,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       FR_SCHED_FENCE();
     }
     __syncthreads();                          // counters dead: the keys reuse their LDS
+    BR_PH();
 #pragma unroll
     for (int k = 0; k < EMAX; ++k)
       if (sl[k] >> 16) fr_scatter_key(bkey, le[k], sl[k] & 0xffff, key[k]);
@@ -575,6 +581,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
       const int n = sl[k] >> 16;
       if (n) le[k] = fr_result(bkey, witems, le[k], sl[k] & 0xffff, n);
     }
+    BR_PH();
   }
   const double den = (double)(nrow - 1);
   const double rden = 1.0 / den;              // (r - 1) / den through mdiv: bit-identical
@@ -742,7 +749,11 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
       wv += __popcll(__ballot(ok));
     }
     {                                         // the next row's loads (clamped to the last row)
+#ifdef FR_DIAG_NOPF
+      const int64_t nxt = row;
+#else
       const int64_t nxt = row + gridDim.x < nrows ? row + gridDim.x : row;
+#endif
 #pragma unroll
       for (int k = 0; k < EMAX; ++k) xv[k] = X[nxt * ld + (fr_ix<NT>(fr_opaque(t), k, (int)A))];
     }
@@ -778,11 +789,13 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
     if (wid == 0) {
       double vmin, vmax;
       fr_key_bounds(h0, h1, &vmin, &vmax);
+      
       fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
     }
     __syncthreads();
     BR_PH();
     int sl[EMAX];
+    
     fr_bucket_cnt<K, EMAX, 4>(tab, key, sl, DUMMY, cnt);
     __syncthreads();
     BR_PH();
@@ -831,6 +844,9 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
     for (int k = 0; k < EMAX; ++k) {
       if (!fr_in<NT>(t, k, (int)A)) continue;
       const uint32_t r2 = ((nan_m >> k) & 1u) ? 0u : (uint32_t)(2 * (sl[k] & 0xffff) + le[k] + 1);
+#ifdef FR_DIAG_NOSTORE
+      if (r2 == 0xfffffu)
+#endif
       __builtin_nontemporal_store((fmx_rank2_t)r2, rk + fr_opaque(t) + k * NT);
     }
     BR_PH();

@@ -28,7 +28,7 @@ def read_phases():
     import ctypes
     lib = _lib.load()
     out = {}
-    for tu in ("cs", "q", "ic"):
+    for tu in ("cs", "hot", "q", "ic"):
         buf = (ctypes.c_ulonglong * 32)()
         getattr(lib, "fmx_debug_phase_" + tu)(buf)
         v = [int(x) for x in buf]
