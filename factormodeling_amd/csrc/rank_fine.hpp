@@ -439,16 +439,39 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     const bool sl = zn.slen <= PW_LDS_MAX;
     if (sl)
       for (int i = t; i < zn.slen; i += NT) zn_sch[i] = g[i];
+    // the rank phase's sample and row bounds now, so that wave 1 builds the splitter table
+    // while wave 0 combines the first moment sum (no serial table phase of its own)
+    fr_park_sample<NT, EMAX>(tab, key);
+    {
+      const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
+      if ((t & 63) == 0) wred[wid] = make_uint4((uint32_t)wp, (uint32_t)wv, a, c);
+    }
     __syncthreads();
     const int32_t* sch = sl ? zn_sch : g;
+    auto table = [&]() {
+      int nv1 = 0;
+      uint32_t a0 = 0xffffffffu, a1 = 0u;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const uint4 r = wred[w];
+        nv1 += (int)r.y;
+        a0 = min(a0, r.z);
+        a1 = max(a1, r.w);
+      }
+      if (nv1 > 0 && An > 1) {                // the rows that rank (dense, method average)
+        double vmin, vmax;
+        fr_key_bounds(a0, a1, &vmin, &vmax);
+        fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
+      }
+    };
 #ifdef FR_DIAG_NOZNSUM
-    int cnt = An; (void)sch;
+    int cnt = An; (void)sch; table();
     const double s1 = vrow[t], mean = s1, s2 = vrow[t + 1], var = s2;
 #else
     int cnt, c2;
     const double s1 = block_pw_sum_w0<NT>([&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; },
                                           [&](int i) { return (int)(vrow[i] == vrow[i]); }, sch, zn_nodes,
-                                          zn_iscr, &cnt);
+                                          zn_iscr, &cnt, table);
     const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
     BR_PH();
     const double s2 = block_pw_sum_w0<NT>([&](int i) {
@@ -475,11 +498,11 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     __syncthreads();                          // every read of the staged row is done
     BR_PH();
   }
-  fr_park_sample<NT, EMAX>(tab, key);
+  if constexpr (!ZN) fr_park_sample<NT, EMAX>(tab, key);
 #pragma unroll
   for (int j = 0; j < WORDS / (4 * NT); ++j)
     reinterpret_cast<uint4*>(cnt)[t * (WORDS / (4 * NT)) + j] = make_uint4(0u, 0u, 0u, 0u);
-  {
+  if constexpr (!ZN) {
     const uint32_t a = fr_wave_min_u32(hmin), c = fr_wave_max_u32(hmax);
     if ((t & 63) == 0) wred[wid] = make_uint4((uint32_t)wp, (uint32_t)wv, a, c);
   }
@@ -527,12 +550,12 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     }
     return;
   }
-  if (wid == 0) {
+  if (!ZN && wid == 0) {                      // (ZN: wave 1 built it during the moments)
     double vmin, vmax;
     fr_key_bounds(h0, h1, &vmin, &vmax);
     fr_build_w0<K>(tab, FR_FROM_LDS, vmin, vmax);
   }
-  __syncthreads();
+  if constexpr (!ZN) __syncthreads();         // (ZN: the counters' zeroing barrier covers it)
   BR_PH();
   int sl[EMAX];                               // slot | bucket << PK_BSHIFT, then start | len << 16
   {

@@ -23,7 +23,8 @@ __global__ void k_ic_empty(double* out, int64_t F, int64_t D, int L0, int L1, in
 
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,
                        const int32_t* lags_host, int n_lags, double* out, hipStream_t st) {
-  const int nt = br_nt(1024);
+  // 512-thread rows up to 4096 assets (C4's 3000: 20.0 vs 23.7 ms per 252 dates)
+  const int nt = br_nt(A <= 4096 ? 512 : 1024);
   // counters, then keys [A] + member info [A] + lag masks [A] (k_ic_daily_fr)
   const size_t lds_fr = std::max<size_t>((size_t)(FRG<FR_K_IC>::NB + 1) * 8, (size_t)A * 13 + 16);
   auto fr_table = FMX_EMAX_TABLE(k_ic_daily_fr);

@@ -92,9 +92,14 @@ __device__ double block_pw_sum(Elem elem, const int32_t* __restrict__ sched, dou
 // rounds (in-order LDS within one wave: no block barrier per round) and publishes the
 // root.  Returns the sum; *count receives the number of valid elements.
 // nodes: >= 2L+1 doubles; iscr: >= NT/64 + 1 ints.
-template <int NT, class Elem, class Valid>
+// side(): run by wave 1 while wave 0 combines (independent work that would otherwise take
+// a serial phase of its own; it must not touch nodes / iscr).
+struct PwNoSide {
+  __device__ void operator()() const {}
+};
+template <int NT, class Elem, class Valid, class Side = PwNoSide>
 __device__ double block_pw_sum_w0(Elem elem, Valid valid, const int32_t* __restrict__ sched, double* nodes,
-                                  int* iscr, int* count) {
+                                  int* iscr, int* count, Side side = Side()) {
   PwView s{sched};
   const int L = s.L(), n = s.n();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -152,6 +157,8 @@ __device__ double block_pw_sum_w0(Elem elem, Valid valid, const int32_t* __restr
       for (int w = 0; w < NT / 64; ++w) tot += iscr[w];
       iscr[NT / 64] = tot;
     }
+  } else if (wid == 1) {
+    side();
   }
   __syncthreads();
   const double r = nodes[0];

@@ -83,7 +83,9 @@ def workload_config(name):
     if name == "c2":
         return StepConfig()
     if name == "c4":
-        return StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None)
+        # the daily IC from one ranks-only pass (cs_rank2 + the wave IC): 15.1 vs 23.7 ms per
+        # 252 dates for the IC kernel that ranks each row itself (profiles/r05)
+        return StepConfig(ops=[], ic_lags=(1,), select=False, gram=True, prune_top_x=None, rank_pass=True)
     if name == "c5":
         return StepConfig(ops=[], ic_lags=(1, 2), select=True, gram=False, ret_ops=[("corr_vol", 60)],
                           factor_chunk=100, composite="zscore", rank_pass=True)
