@@ -107,7 +107,8 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   // block.  Dynamic LDS: ICW_WAVES * 2 * (nbp + ICW_EC) words.
   extern __shared__ uint32_t icw_lds[];
   __shared__ double scr[ICW_WAVES * 32];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // the wave index as a scalar: the row, its pointers and lags live in SGPRs (saddr loads)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t row = (int64_t)blockIdx.x * ICW_WAVES + wid;
   if (row >= F * D) return;                   // whole waves; no workgroup barrier below
   const int64_t s = row / F, f = row % F;
@@ -144,13 +145,21 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   const int An = (int)A;
   double xq[ICW_PF], rq[ICW_PF][2];
   uint32_t kq[ICW_PF];
+  // an inactive lag reads the row's own date (rr clamped above): its sums are never written
   auto load = [&](int i0, int s) {
     const int i = i0 + lane;
-    const bool in = i < An;
-    xq[s] = in ? xf[i] : qnan();
-    kq[s] = in ? (uint32_t)rkf[i] : 0u;
+    if (i0 + 64 <= An) {                      // wave-uniform: every chunk but a ragged last
+      xq[s] = xf[i];
+      kq[s] = (uint32_t)rkf[i];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) rq[s][m] = (in && act[m]) ? rr[m][i] : qnan();
+      for (int m = 0; m < 2; ++m) rq[s][m] = rr[m][i];
+    } else {
+      const bool in = i < An;
+      xq[s] = in ? xf[i] : qnan();
+      kq[s] = in ? (uint32_t)rkf[i] : 0u;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) rq[s][m] = in ? rr[m][i] : qnan();
+    }
   };
 #pragma unroll
   for (int s = 0; s < ICW_PF; ++s) load(64 * s, s);
@@ -245,11 +254,15 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     for (int q = 0; q < 6; ++q) sm[m][q] = 0.0;
   // software pipeline, ICW_PF chunks deep: the loads of chunks i+1..i+ICW_PF are in flight
   // while chunk i is reduced (one wave per row: without it every chunk waits a full HBM
-  // latency and only other waves hide it); the first ICW_PF were issued before step 1
-  for (int i0 = 0; i0 < An; i0 += 64) {
-    const double x = xq[0];
-    const uint32_t rk = kq[0];
-    double r[2] = {rq[0][0], rq[0][1]};
+  // latency and only other waves hide it); the first ICW_PF were issued before step 1.
+  // Two loops over the same pipeline: the first runs until every active lag has its shift
+  // (usually chunk 0), the second -- the hot one -- carries no shift bookkeeping, so the
+  // pair masks stay wave masks (no booleans materialised across the shift block).
+  auto next = [&](int i0, double& x, uint32_t& rk, double (&r)[2]) {
+    x = xq[0];
+    rk = kq[0];
+    r[0] = rq[0][0];
+    r[1] = rq[0][1];
 #pragma unroll
     for (int s = 0; s + 1 < ICW_PF; ++s) {   // rotate (register renames)
       xq[s] = xq[s + 1];
@@ -258,43 +271,68 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
       rq[s][1] = rq[s + 1][1];
     }
     if (i0 + 64 * ICW_PF < An) load(i0 + 64 * ICW_PF, ICW_PF - 1);
+  };
+  auto accum = [&](int m, bool p, uint64_t bp, double x, uint32_t rk, double r) {
+    // difference flags as wave masks: compares straight into scalar masks, ANDed with the
+    // pair mask bp (a short-circuit p && ... would materialise the booleans in VGPRs)
+    dm[2 * m] |= bp & __ballot(x != ax[m]);
+    dm[2 * m + 1] |= bp & __ballot(r != ar[m]);
+    if (!p) return;
+    int corr = 0;
+    if (ne[m]) {                              // wave-uniform
+      const uint32_t tb = T[m][rk >> 6];
+      const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16;
+      corr = 2 * (int)j0;
+      for (uint32_t j = j0; j < j1; ++j) {    // this block's entries (usually none)
+        const uint32_t e = eb[m][j];
+        corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
+      }
+    }
+    const uint32_t k2 = rk - (uint32_t)corr;
+    const double dx = x - ax[m], dy = r - ar[m];
+    // the moment sums with fused multiply-adds: the records are tolerance-pinned (single-pass
+    // moments about the first pair, ~1e-15 relative), not bit-pinned, and an fma per term is
+    // both one instruction and one rounding fewer
+    sm[m][0] += dx; sm[m][1] += dy;
+    sm[m][2] = __builtin_fma(dx, dx, sm[m][2]);
+    sm[m][3] = __builtin_fma(dy, dy, sm[m][3]);
+    sm[m][4] = __builtin_fma(dx, dy, sm[m][4]);
+    sm[m][5] = __builtin_fma((double)k2, dy, sm[m][5]);
+    kk[m] += (uint64_t)k2 * k2;
+  };
+  // an inactive lag needs no shift (its records are never written)
+  ref[0] = !act[0];
+  ref[1] = !act[1];
+  int i0 = 0;
+  for (; i0 < An && !(ref[0] && ref[1]); i0 += 64) {
+    double x, r[2];
+    uint32_t rk;
+    next(i0, x, rk, r);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      const bool p = x == x && r[m] == r[m];
+      const bool p = (x == x) & (r[m] == r[m]);
       const uint64_t bp = __ballot(p);
-      if (!bp) continue;
       cnt[m] += __popcll(bp);
-      if (!ref[m]) {                          // wave-uniform: the first chunk with pairs
+      if (!ref[m] && bp) {                    // wave-uniform: the first chunk with pairs
         const int l = __ffsll((unsigned long long)bp) - 1;
         ax[m] = fr_readlane_d(x, l);
         ar[m] = fr_readlane_d(r[m], l);
         ref[m] = true;
       }
-      // difference flags as wave masks, in wave-uniform control flow (scalar ORs)
-      dm[2 * m] |= __ballot(p && x != ax[m]);
-      dm[2 * m + 1] |= __ballot(p && r[m] != ar[m]);
-      if (!p) continue;
-      int corr = 0;
-      if (ne[m]) {
-        const uint32_t tb = T[m][rk >> 6];
-        const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16;
-        corr = 2 * (int)j0;
-        for (uint32_t j = j0; j < j1; ++j) {  // this block's entries (usually none)
-          const uint32_t e = eb[m][j];
-          corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
-        }
-      }
-      const uint32_t k2 = rk - (uint32_t)corr;
-      const double dx = x - ax[m], dy = r[m] - ar[m];
-      // the moment sums with fused multiply-adds: the records are tolerance-pinned (single-pass
-      // moments about the first pair, ~1e-15 relative), not bit-pinned, and an fma per term is
-      // both one instruction and one rounding fewer
-      sm[m][0] += dx; sm[m][1] += dy;
-      sm[m][2] = __builtin_fma(dx, dx, sm[m][2]);
-      sm[m][3] = __builtin_fma(dy, dy, sm[m][3]);
-      sm[m][4] = __builtin_fma(dx, dy, sm[m][4]);
-      sm[m][5] = __builtin_fma((double)k2, dy, sm[m][5]);
-      kk[m] += (uint64_t)k2 * k2;
+      if (ref[m]) accum(m, p, bp, x, rk, r[m]);   // before the shift: no pairs to add
+    }
+  }
+  for (; i0 < An; i0 += 64) {
+    double x, r[2];
+    uint32_t rk;
+    next(i0, x, rk, r);
+    const bool xo = x == x;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const bool p = xo & (r[m] == r[m]);
+      const uint64_t bp = __ballot(p);
+      cnt[m] += __popcll(bp);
+      accum(m, p, bp, x, rk, r[m]);
     }
   }
   // 3. butterflies into the wave's scratch: [0,6) lag 0's sums, [6,12) lag 1's, [12,14) the
