@@ -25,6 +25,7 @@ namespace fmx {
 static_assert(EX_SLOTS == FMX_GRAM_EXACT_SLOTS, "exact Gram limb layout");
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef float flt16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -496,33 +497,44 @@ __host__ __device__ inline int64_t unit_chunk(int64_t u, int S, int64_t nch) {
   return (u / S) * nch + ((u % S) * nch) / S;
 }
 
+// k_gram_db: 16 waves (4 per SIMD, 128 registers each; 12 waves with 168: 12.97 vs 12.09 ms
+// at C2 -- the fourth wave per SIMD hides more of the fragment reads than the registers buy)
+#ifndef GDB_NT
+#define GDB_NT 1024
+#endif
+#ifndef GDB_FENCE
+#define GDB_FENCE 1
+#endif
 #ifndef GDB_PAD
 #define GDB_PAD 1      // k_gram_db k-steps without the per-block branch (dummy block for short waves; 0: A/B arm, +0.4 ms at C2)
 #endif
 template <int NB, bool ZIN, bool UNITS = false>   // ZIN: X holds the z-scores (cs_zscore output), stats unused
-__global__ void __launch_bounds__(SG_NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
+__global__ void __launch_bounds__(GDB_NT) __attribute__((amdgpu_waves_per_eu(GDB_NT / 256, GDB_NT / 256)))
 k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_t F, int64_t D, int64_t A,
           int64_t ld, int64_t d0, int64_t nch, int64_t total, int64_t nslice, double* __restrict__ part,
           uint32_t* __restrict__ mbits, int opt, int units_per_date = 1) {
   constexpr int FP = 16 * NB;
   constexpr int NTRI = NB * (NB + 1) / 2;
-  constexpr int NWV = SG_NT / 64;
+  constexpr int NWV = GDB_NT / 64;
   constexpr int BPW = (NTRI + NWV - 1) / NWV;
   constexpr int NEL = FP * SG_K;
-  constexpr int EPT = (NEL + SG_NT - 1) / SG_NT;
+  constexpr int EPT = (NEL + GDB_NT - 1) / GDB_NT;
   __shared__ double Zs[2][FP * SG_KP];
   __shared__ double mu_s[2][FP], sd_s[2][FP];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // the wave index as a scalar: block ids, fragment rows and the A-row test in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t slice = blockIdx.x;
   // UNITS: ``total`` counts units; the slice's chunk range is its units' (contiguous) chunks
   const int S = units_per_date;
   const int64_t u0 = slice * total / nslice, u1 = (slice + 1) * total / nslice;
   const int64_t c0 = UNITS ? unit_chunk(u0, S, nch) : u0, c1 = UNITS ? unit_chunk(u1, S, nch) : u1;
   int64_t cur_u = u0, u_end = UNITS ? unit_chunk(u0 + 1, S, nch) : 0;
+  // wave w owns the BPW consecutive triangle blocks [BPW w, BPW w + BPW) (row-major): most
+  // of them share their block row, whose A fragment is then read once per k-step pair
   int blk[BPW];
 #pragma unroll
   for (int u = 0; u < BPW; ++u) {
-    int j = wid + NWV * u, bi = 0;
+    int j = BPW * wid + u, bi = 0;
     blk[u] = -1;
     if (j < NTRI) {
       while (j >= NB - bi) { j -= NB - bi; ++bi; }
@@ -537,7 +549,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   int64_t ld_d = c0 / nch, ld_a = c0 - (c0 / nch) * nch;
   // one 64-bit row address per issue, made opaque so the compiler cannot hoist the EPT
   // per-element row offsets out of the chunk loop (they spilled, and every reload's
-  // vmcnt(0) wait serialised the chunk's loads); element u is SG_NT / 32 rows further on
+  // vmcnt(0) wait serialised the chunk's loads); element u is GDB_NT / 32 rows further on
   auto issue = [&]() {
     const int64_t d = d0 + ld_d, a0 = ld_a * SG_K;
     if (++ld_a == nch) { ld_a = 0; ++ld_d; }
@@ -545,17 +557,17 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
     const int64_t a = a0 + cl;
     const double* xb = X + ((int64_t)r0 * D + d) * ld + a;
     asm volatile("" : "+v"(xb));
-    const int64_t step = (int64_t)(SG_NT / 32) * D * ld;
+    const int64_t step = (int64_t)(GDB_NT / 32) * D * ld;
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
-      const int e = tid + SG_NT * u, r = r0 + (SG_NT / 32) * u;
+      const int e = tid + GDB_NT * u, r = r0 + (GDB_NT / 32) * u;
       xr[u] = (e < NEL && r < F && a < A) ? xb[u * step] : qnan();
     }
   };
   auto load_stats = [&](int64_t dr) {             // date d0 + dr into buffer dr & 1
     if (ZIN) return;
     const int p = (int)(dr & 1);
-    for (int r = tid; r < FP; r += SG_NT) {
+    for (int r = tid; r < FP; r += GDB_NT) {
       mu_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr)] : 0.0;
       sd_s[p][r] = r < F ? stats[2 * ((int64_t)r * D + d0 + dr) + 1] : 0.0;
     }
@@ -565,7 +577,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
     const int p = (int)(dr & 1);
 #pragma unroll
     for (int u = 0; u < EPT; ++u) {
-      const int e = tid + SG_NT * u, r = e >> 5, cl = e & 31;
+      const int e = tid + GDB_NT * u, r = e >> 5, cl = e & 31;
       if (e >= NEL) continue;                     // wave-uniform (NEL is a multiple of 64)
       const double v = xr[u];
       bool ok;
@@ -599,6 +611,9 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
   for (int64_t c = c0; c < c1; ++c) {
     const int b = (int)((c - c0) & 1);
     auto next = [&]() {
+#ifdef GDB_DIAG_NOSTAGE
+      return;                                     // diagnostic (wrong results): MFMAs only
+#endif
       if (c + 1 < c1) {
         const int64_t dn = (c + 1) / nch;         // date of chunk c + 1
         stage(c + 1, dn, b ^ 1);                  // its stats were loaded a date ahead
@@ -609,9 +624,15 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
       }
     };
     if (!mfma_first) next();
+    // two k-steps per iteration: lane group g = lane >> 4 takes the chunk's k = ks + 2g and
+    // ks + 2g + 1 in the two steps, so each fragment pair is ONE ds_read_b128 (the A and B
+    // operands use the same k map, and every k of the chunk is taken once: the sum is the
+    // same, only the MFMAs' accumulation order is fixed differently)
 #pragma unroll 1
-    for (int ks = 0; ks < SG_K; ks += 4) {
-      const int kk = ks + (lane >> 4);
+    for (int ks = 0; ks < SG_K; ks += 8) {
+      const int kk = ks + 2 * (lane >> 4);
+      int abi = -1;
+      dbl2 a = dbl2{0.0, 0.0};
 #pragma unroll
       for (int u = 0; u < BPW; ++u) {
 #if GDB_PAD
@@ -624,9 +645,17 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
         const int bk = blk[u];
 #endif
         const int bi = bk & 0xff, bj = bk >> 8;
-        const double a = Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk];
-        const double bb = Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk];
-        gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, gacc[u], 0, 0, 0);
+        if (bi != abi) {                          // wave-uniform: a new block row
+          a = *reinterpret_cast<const dbl2*>(&Zs[b][(bi * 16 + (lane & 15)) * SG_KP + kk]);
+          abi = bi;
+        }
+        // (reading the next block's fragments ahead of these MFMAs: 12.67 vs 12.13 ms)
+        const dbl2 bb = *reinterpret_cast<const dbl2*>(&Zs[b][(bj * 16 + (lane & 15)) * SG_KP + kk]);
+        gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, bb.x, gacc[u], 0, 0, 0);
+        gacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, bb.y, gacc[u], 0, 0, 0);
+#if GDB_FENCE
+        __builtin_amdgcn_sched_barrier(0);        // bounds the fragments in flight (VGPRs)
+#endif
       }
     }
     if (UNITS) {
@@ -635,7 +664,7 @@ k_gram_db(const double* __restrict__ X, const double* __restrict__ stats, int64_
 #pragma unroll
         for (int u = 0; u < BPW; ++u) {
           if (blk[u] < 0) continue;
-          *reinterpret_cast<dbl4*>(pu + (int64_t)(wid + NWV * u) * 256) = gacc[u];
+          *reinterpret_cast<dbl4*>(pu + (int64_t)(BPW * wid + u) * 256) = gacc[u];
           gacc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
         }
         if (++cur_u >= u1) break;
@@ -848,10 +877,10 @@ static fmx_status gram_small_launch(const double* X, const double* stats, double
     // bit 1: MFMA / staging interleave across each SIMD's waves (default; A/B switch)
     static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
     if (stats)
-      k_gram_db<NB, false><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
+      k_gram_db<NB, false><<<(unsigned)nslice, GDB_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
                                                               mbits, gopt);
     else
-      k_gram_db<NB, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
+      k_gram_db<NB, true><<<(unsigned)nslice, GDB_NT, 0, st>>>(X, stats, F, D, A, ld, d0, nch, nw, nslice, part,
                                                              mbits, gopt);
     FMX_LAUNCH_CHECK("k_gram_db");
   } else {
@@ -924,10 +953,10 @@ static fmx_status gram_exact_launch(const double* X, const double* stats, int64_
   const int64_t nslice = std::max<int64_t>(1, std::min<int64_t>(pl.nunits, cus));
   static const int gopt = getenv("FMX_GRAM_OPT") ? atoi(getenv("FMX_GRAM_OPT")) : 2;
   if (stats)
-    k_gram_db<NB, false, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
+    k_gram_db<NB, false, true><<<(unsigned)nslice, GDB_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
                                                                     nslice, part, mbits, gopt, (int)pl.S);
   else
-    k_gram_db<NB, true, true><<<(unsigned)nslice, SG_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
+    k_gram_db<NB, true, true><<<(unsigned)nslice, GDB_NT, 0, st>>>(X, stats, F, D, A, ld, d0, pl.nch, pl.nunits,
                                                                    nslice, part, mbits, gopt, (int)pl.S);
   FMX_LAUNCH_CHECK("k_gram_db<units>");
   {
