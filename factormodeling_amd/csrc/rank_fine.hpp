@@ -734,6 +734,9 @@ __device__ __forceinline__ void fr_bucket_cnt(const FrTab& T, const uint64_t* ke
 // per CU at 64 VGPRs spilled the keys).  Bucket pipeline and per-element results as
 // k_cs_rank_fa (dense, method average, RK only):
 //   rank2 = 2 * #less + #equal + 1 (0 for NaN); single-asset rows -> 2.
+#ifndef FR_PF_LISTS
+#define FR_PF_LISTS 0
+#endif
 template <int NT, int EMAX>
 __global__ void __launch_bounds__(NT, 4)
 k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld, fmx_rank2_t* __restrict__ RK,
@@ -824,6 +827,7 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
     BR_PH();
     fr_scan16<NT, WORDS>(cnt, iscr);
     BR_PH();
+#if FR_PF_LISTS
     int le[EMAX];                             // work item / slot, then c = 2 #less + #equal in the bucket
     uint32_t nan_m = 0;
     const int wcap = lcap / NW;
@@ -863,6 +867,49 @@ k_cs_rank2_pf(const double* __restrict__ X, int64_t nrows, int64_t A, int64_t ld
         le[k] = 2 * (c & 0xffff) + (c >> 16);
       }
     }
+#else
+    // in-bucket scans as per-slot loops (each element walks its own bucket): at one 1024-thread
+    // row per CU the per-wave work lists of k_cs_rank_fa cost more than they balance
+    // (C5 rank pass 115.5 vs 104.3 ms)
+    int le[EMAX];                             // scatter slot, then c = 2 #less + #equal in the bucket
+    uint32_t nan_m = 0;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
+      const int slot = sl[k] & PK_SLOT;
+      int s0, s1;
+      fr_cnt_get2(cnt, b, &s0, &s1);
+      const int n = s1 - s0;
+      const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
+      const bool scan = !eqb && n > 1 && b != DUMMY;
+      nan_m |= (uint32_t)(b == DUMMY) << k;
+      le[k] = scan ? slot : (eqb ? n : 1);
+      sl[k] = s0 | (scan ? n << 16 : 0);
+    }
+    __syncthreads();                          // counters dead: the keys reuse their LDS
+    BR_PH();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (sl[k] >> 16) bkey[(sl[k] & 0xffff) + le[k]] = key[k];
+    __syncthreads();
+    BR_PH();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int n = sl[k] >> 16;
+      if (n) {
+        const uint64_t* bk = bkey + (sl[k] & 0xffff);
+        const uint64_t own = bk[le[k]];       // own key from its slot: keys dead after the scatter
+        int c = 0;
+#pragma unroll 2
+        for (int j = 0; j < n; ++j) {
+          const uint64_t w = bk[j];
+          c += (w < own ? 2 : 0) + (w == own ? 1 : 0);
+        }
+        le[k] = c;
+      }
+    }
+    BR_PH();
+#endif
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       if (!fr_in<NT>(t, k, (int)A)) continue;
