@@ -364,6 +364,9 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
 // sum of squared deviations (block_pw_sum_w0, bit-identical to k_cs_moment_rg), and the two
 // outputs are written from it before the ranking starts: the row is read from HBM once for
 // four operators (fmx_cs_rank_winsor_zn).
+#ifndef FR_FA_LISTS
+#define FR_FA_LISTS 0
+#endif
 template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false, bool ZN = false>
 __global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
@@ -569,9 +572,14 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   fr_scan16<NT, WORDS>(cnt, iscr);
   BR_PH();
   // le[k] = #less | #equal << 16 inside the bucket; for elements still to scan (n field of
-  // sl set) first their work item in the wave's list region (fr_claim_put)
+  // sl set) first their work item in the wave's list region (fr_claim_put).  Per-wave work
+  // lists for long rows and the winsor passes, per-slot loops for short rank-only rows
+  // (measured per 252 dates: A = 5000 cs_rank 1.60 vs 1.68 ms, cs_rank_winsor 2.13 vs 2.30
+  // with lists; A = 3000 cs_rank 9.42 vs 10.13 ms and the C4 rank pass 9.38 vs 10.04 with
+  // per-slot loops, its cs_rank_winsor 12.11 vs 12.29 with lists).  FR_FA_LISTS=1: lists
+  // everywhere (A/B)
   int le[EMAX];
-  {
+  if constexpr (ZN || WQ || EMAX >= 8 || FR_FA_LISTS) {
     const int wcap = lcap / NW;
     uint32_t* witems = litems + wid * wcap;
     FrClaim lcl;
@@ -603,6 +611,44 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     for (int k = 0; k < EMAX; ++k) {
       const int n = sl[k] >> 16;
       if (n) le[k] = fr_result(bkey, witems, le[k], sl[k] & 0xffff, n);
+    }
+    BR_PH();
+  } else {
+    (void)lcap;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int b = (sl[k] >> PK_BSHIFT) & (FR_BEQ - 1);
+      const int slot = sl[k] & PK_SLOT;
+      int s0, s1;
+      fr_cnt_get2(cnt, b, &s0, &s1);
+      const int n = s1 - s0;
+      const bool eqb = (sl[k] >> PK_BSHIFT) & FR_BEQ;   // equal-to-sample bucket: all members tie
+      const bool scan = !eqb && n > 1 && b != DUMMY;
+      le[k] = scan ? slot : (eqb ? n : 1) << 16;
+      sl[k] = s0 | (scan ? n << 16 : 0);
+    }
+    __syncthreads();                          // counters dead: the keys reuse their LDS
+    BR_PH();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k)
+      if (sl[k] >> 16) bkey[(sl[k] & 0xffff) + le[k]] = key[k];
+    __syncthreads();
+    BR_PH();
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const int n = sl[k] >> 16;
+      if (n) {
+        const uint64_t* bk = bkey + (sl[k] & 0xffff);
+        const uint64_t own = bk[le[k]];       // own key from its slot: keys dead after the scatter
+        int lt = 0, eq = 0;
+#pragma unroll 2
+        for (int j = 0; j < n; ++j) {
+          const uint64_t w = bk[j];
+          lt += w < own ? 1 : 0;
+          eq += w == own ? 1 : 0;
+        }
+        le[k] = lt | eq << 16;
+      }
     }
     BR_PH();
   }
