@@ -40,6 +40,9 @@ SIGNATURES = {
     "fmx_group_rank_sorted": [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     "fmx_group_rank_sorted_work_bytes": [c_i64, c_i64, c_i64],
     "fmx_cs_rank2": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp],
+    "fmx_cs_rank_winsor_zn_dates": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_dbl,
+                                    c_dbl, c_vp, c_vp],
+    "fmx_cs_rank2_dates": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp],
     "fmx_cs_rank": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_cs_winsor": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],
     "fmx_cs_filter_center": [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_dbl, c_dbl, c_vp, c_vp],

@@ -955,7 +955,7 @@ extern "C" fmx_status fmx_cs_rank_winsor_zn(const double* X, double* Yrank, doub
   fmx_status e = FMX_OK;
   PwTable pw = pw_table((int)A, &e);
   if (e) return e;
-  e = br_cs_rank_winsor_zn(X, Yrank, Ywinsor, Yz, Yn, F, D, A, ld, qlo, qhi, rank2, pw, pw_len((int)A),
+  e = br_cs_rank_winsor_zn(X, Yrank, Ywinsor, Yz, Yn, F, D, A, ld, 0, D, qlo, qhi, rank2, pw, pw_len((int)A),
                            as_stream(stream));
   if (e != FMX_ERR_UNSUPPORTED) return e;
   // rows the fused kernel does not take: rank + winsor, then the moments
@@ -968,7 +968,40 @@ extern "C" fmx_status fmx_cs_rank2(const double* X, fmx_rank2_t* rank2, int64_t 
   FMX_ARG(X && rank2, "null panel");
   FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
-  return br_cs_rank2(X, rank2, F, D, A, ld, as_stream(stream));
+  return br_cs_rank2(X, rank2, F, D, A, ld, 0, D, as_stream(stream));
+}
+
+// Date sub-ranges [d0, d1) of every factor of an [F][D][ld] panel (the sharded step: the
+// owned dates before the halo exchange lands, the halo rows after it).  Fine-bucket rows only.
+extern "C" fmx_status fmx_cs_rank_winsor_zn_dates(const double* X, double* Yrank, double* Ywinsor, double* Yz,
+                                                  double* Yn, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0,
+                                                  int64_t d1, double qlo, double qhi, fmx_rank2_t* rank2,
+                                                  void* stream) {
+  FMX_ARG(X && Yrank && Ywinsor && Yz && Yn, "null panel");
+  const double* outs[4] = {Yrank, Ywinsor, Yz, Yn};
+  for (int i = 0; i < 4; ++i) {
+    FMX_ARG(outs[i] != X, "outputs must be distinct from X");
+    for (int j = i + 1; j < 4; ++j) FMX_ARG(outs[i] != outs[j], "outputs must be distinct from each other");
+  }
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
+  FMX_ARG(0 <= d0 && d0 <= d1 && d1 <= D, "date range outside the panel");
+  if (F == 0 || d1 == d0 || A == 0) return FMX_OK;
+  fmx_status e = FMX_OK;
+  PwTable pw = pw_table((int)A, &e);
+  if (e) return e;
+  e = br_cs_rank_winsor_zn(X, Yrank, Ywinsor, Yz, Yn, F, D, A, ld, d0, d1, qlo, qhi, rank2, pw, pw_len((int)A),
+                           as_stream(stream));
+  if (e == FMX_ERR_UNSUPPORTED) set_error("fmx_cs_rank_winsor_zn_dates: rows of the fine-bucket kernel only");
+  return e;
+}
+
+extern "C" fmx_status fmx_cs_rank2_dates(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A,
+                                         int64_t ld, int64_t d0, int64_t d1, void* stream) {
+  FMX_ARG(X && rank2, "null panel");
+  FMX_ARG(F >= 0 && D >= 0 && A >= 0 && ld >= A && A <= 16384, "bad dims (A <= 16384)");
+  FMX_ARG(0 <= d0 && d0 <= d1 && d1 <= D, "date range outside the panel");
+  if (F == 0 || d1 == d0 || A == 0) return FMX_OK;
+  return br_cs_rank2(X, rank2, F, D, A, ld, d0, d1, as_stream(stream));
 }
 
 extern "C" fmx_status fmx_cs_filter_center(const double* X, double* Y, int64_t F, int64_t D, int64_t A,

@@ -397,7 +397,9 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     rw = fr_ic_row(ic, D);
     if (t < 2) ic_ne[t] = 0;
   }
-  const int64_t row = IC ? rw.f * D + rw.s : fmx_blk();   // grid dim3(D, F)
+  // grid dim3(dates, F): row (f, d) = f * D + x, the panel pointers offset by the range's
+  // first date (a date sub-range: the sharded step's owned dates, fmx_*_dates)
+  const int64_t row = IC ? rw.f * D + rw.s : (int64_t)blockIdx.y * D + blockIdx.x;
   const double* x = X + row * ld;
   double* y = Y + row * ld;
   const uint8_t* prow = PRES ? present + (row % D) * ld : nullptr;

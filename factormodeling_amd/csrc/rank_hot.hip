@@ -12,16 +12,21 @@ template <int NT, int E> constexpr auto kcr_dense_h = k_cs_rank_fa<NT, E, false>
 // cs_rank + cs_winsor (+ doubled ranks) + cs_zscore + market_neutralize of dense rows in one
 // pass (k_cs_rank_fa<ZN>); FMX_ERR_UNSUPPORTED when the row does not fit the fine kernel.
 template <int NT, int E> constexpr auto kcrwz_dense = k_cs_rank_fa<NT, E, false, true, false, true>;
+// Rows of dates [d0, d1) of every factor (the panel keeps its D dates; the kernel maps
+// grid x to date d0 + x through pointers offset by d0 rows).
 fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double* Yz, double* Yn, int64_t F, int64_t D,
-                                int64_t A, int64_t ld, double qlo, double qhi, fmx_rank2_t* RK, PwTable pw, int slen,
-                                hipStream_t st) {
+                                int64_t A, int64_t ld, int64_t d0, int64_t d1, double qlo, double qhi,
+                                fmx_rank2_t* RK, PwTable pw, int slen, hipStream_t st) {
   const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcrwz_dense)(nt_fa, E);
   if (rank_impl() == RANK_IMPL_BR || !k || !lds_fits(k, lds_fr)) return FMX_ERR_UNSUPPORTED;
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
-  if (F * D == 0) return FMX_OK;
+  if (F * (d1 - d0) == 0) return FMX_OK;
+  const int64_t off = d0 * ld;
+  X += off; Yr += off; Yw += off; Yz += off; Yn += off;
+  if (RK) RK += off;
   int method = FMX_RANK_AVERAGE;
   const uint8_t* present = nullptr;
   FrIc ic{};
@@ -32,7 +37,7 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(d1 - d0, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 
@@ -48,11 +53,13 @@ static bool rank2_pf_enabled() {
   return v;
 }
 
-fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st) {
+fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0,
+                       int64_t d1, hipStream_t st) {
   const int nt_fa = fa_nt(A) == 1024 ? 1024 : 512;
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
-  if (nt_fa == 1024 && E == 10 && rank_impl() == RANK_IMPL_FINE && rank2_pf_enabled()) {
+  const bool whole = d0 == 0 && d1 == D;      // the persistent kernel walks whole panels
+  if (whole && nt_fa == 1024 && E == 10 && rank_impl() == RANK_IMPL_FINE && rank2_pf_enabled()) {
     int64_t nrows = F * D;
     const void* kp = (const void*)k_cs_rank2_pf<1024, 10>;
     const FrListLds ll = fr_list_lds(kp, A, (size_t)fr_list_off(A, FR_CS_WORDS), 0);
@@ -63,7 +70,9 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcr_dense_h)(nt_fa, E);
   if (!k || !lds_fits(k, lds_fr)) { set_error("fmx_cs_rank2: A <= 16384"); return FMX_ERR_UNSUPPORTED; }
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
-  if (F * D == 0) return FMX_OK;
+  if (F * (d1 - d0) == 0) return FMX_OK;
+  X += d0 * ld;
+  RK += d0 * ld;
   double* Y = nullptr;
   double* Y2 = nullptr;
   int method = FMX_RANK_AVERAGE;
@@ -76,7 +85,7 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
-  FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
+  FMX_HIP(hipLaunchKernel(k, fmx_grid2(d1 - d0, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
 

@@ -336,9 +336,10 @@ bool gram_zc_fits(int64_t A);
 fmx_status gram_zc_pass(const double* X, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t dc0, int64_t ndc,
                         double* Zc, int64_t apad, uint32_t* bits, int64_t nd_all, int64_t nwd, void* stream);
 fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double* Yz, double* Yn, int64_t F, int64_t D,
-                                int64_t A, int64_t ld, double qlo, double qhi, fmx_rank2_t* RK, PwTable pw, int slen,
-                                hipStream_t st);
-fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, hipStream_t st);
+                                int64_t A, int64_t ld, int64_t d0, int64_t d1, double qlo, double qhi,
+                                fmx_rank2_t* RK, PwTable pw, int slen, hipStream_t st);
+fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0,
+                       int64_t d1, hipStream_t st);
 fmx_status br_cs_quantile(int op, const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld,
                           double qlo, double qhi, const uint8_t* present, hipStream_t st);
 fmx_status br_ic_daily(const double* X, const double* R, int64_t F, int64_t D, int64_t A, int64_t ld,

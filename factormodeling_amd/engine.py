@@ -241,10 +241,12 @@ def cs_rank_winsor(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, presen
 
 
 def cs_rank_winsor_zn(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, out_zscore=None, out_neutralize=None,
-                      rank2=None):
+                      rank2=None, dates=None):
     """cs_rank(average), cs_winsor(qlo, qhi), cs_zscore and market_neutralize of the same
     dense rows in one pass (fmx_cs_rank_winsor_zn: each row read once); every output is
     bit-identical to its own kernel.  ``rank2``: also the doubled ranks (as cs_rank_winsor).
+    ``dates`` = (d0, d1): only the rows of those dates (fmx_cs_rank_winsor_zn_dates; the other
+    rows of the outputs are left as they are; A <= 16384).
     Returns (Yrank, Ywinsor, Yzscore, Yneutralize)."""
     X = as3(X)
     _check_panel(X)
@@ -253,6 +255,11 @@ def cs_rank_winsor_zn(X, qlo=0.01, qhi=0.99, out_rank=None, out_winsor=None, out
     if rank2 is not None:
         if rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
             raise _lib.FmxError("rank2 must be a contiguous int16 (bit pattern uint16) [F][D][A] tensor")
+    if dates is not None:
+        d0, d1 = (int(d) for d in dates)
+        call("fmx_cs_rank_winsor_zn_dates", ptr(X), *[ptr(o) for o in outs], F, D, A, A, d0, d1, float(qlo),
+             float(qhi), ptr(rank2), stream_ptr())
+        return tuple(outs)
     if A > FINE_RANK_MAX_A and rank2 is None:
         cs_rank_winsor(X, qlo, qhi, outs[0], outs[1])
         cs_zscore_neutralize(X, outs[2], outs[3])
@@ -292,9 +299,10 @@ def cs_rank_winsor_ic(X, R, lags=(1, 2), qlo=0.01, qhi=0.99, out_rank=None, out_
     return Yr, Yw, out
 
 
-def cs_rank2(X, rank2=None):
+def cs_rank2(X, rank2=None, dates=None):
     """Doubled average ranks only (fmx_cs_rank2): the rank pass ``ic_daily(..., rank2=)``
-    starts from when no operator output of the rows is wanted (dense rows, A <= 16384)."""
+    starts from when no operator output of the rows is wanted (dense rows, A <= 16384).
+    ``dates`` = (d0, d1): only the rows of those dates (fmx_cs_rank2_dates)."""
     X = as3(X)
     _check_panel(X)
     F, D, A = X.shape
@@ -302,6 +310,10 @@ def cs_rank2(X, rank2=None):
         rank2 = torch.empty((F, D, A), dtype=RANK2_DTYPE, device=X.device)
     elif rank2.dtype != RANK2_DTYPE or tuple(rank2.shape) != (F, D, A) or not rank2.is_contiguous():
         raise _lib.FmxError("rank2 must be a contiguous int16 [F][D][A] tensor")
+    if dates is not None:
+        d0, d1 = (int(d) for d in dates)
+        call("fmx_cs_rank2_dates", ptr(X), ptr(rank2), F, D, A, A, d0, d1, stream_ptr())
+        return rank2
     call("fmx_cs_rank2", ptr(X), ptr(rank2), F, D, A, A, stream_ptr())
     return rank2
 

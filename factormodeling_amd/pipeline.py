@@ -305,9 +305,13 @@ class EngineBackend:
         E.cs_rank_winsor(X, 0.01, 0.99, outs[0], outs[1], rank2=rank2)
 
     @staticmethod
-    def cs_rank_winsor_zn(X, outs, rank2=None):
-        """cs_rank, cs_winsor, cs_zscore and market_neutralize of the rows in one pass."""
-        E.cs_rank_winsor_zn(X, 0.01, 0.99, *outs, rank2=rank2)
+    def cs_rank_winsor_zn(X, outs, rank2=None, dates=None):
+        """cs_rank, cs_winsor, cs_zscore and market_neutralize of the rows in one pass
+        (``dates`` = (d0, d1): only those dates' rows)."""
+        E.cs_rank_winsor_zn(X, 0.01, 0.99, *outs, rank2=rank2, dates=dates)
+
+    # the fused pass and the ranks-only pass take date sub-ranges (the sharded step's plan)
+    zn_dates = True
 
     ranked_ic_max_a = E.RANKED_IC_MAX_A
 
@@ -317,9 +321,9 @@ class EngineBackend:
     rank_pass_max_a = int(os.environ.get("FMX_RANK_PASS_MAX_A", "16384"))
 
     @staticmethod
-    def cs_rank2(X, rank2):
+    def cs_rank2(X, rank2, dates=None):
         """The doubled ranks alone (no operator output): the IC's rank pass."""
-        E.cs_rank2(X, rank2)
+        E.cs_rank2(X, rank2, dates=dates)
 
     # the daily IC fused into the rank pass (fmx_cs_rank_winsor_ic: the ranks never leave
     # the CU).  Off by default: at C2 it measured 37.4 ms against 21.1 + 8.8 ms for the rank
@@ -473,7 +477,15 @@ def _run_stage(name, ops, outs, X, be, side, timers, collect, own):
             if rk is None or tuple(rk.shape) != tuple(X.shape):
                 rk = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=X.device)
             side["rank2"] = rk
-        be.cs_rank_winsor_zn(X, outs, rank2=rk)
+        zd = side.get("zn_dates") if side is not None else None
+        if zd is not None:
+            # sharded: the owned dates now (the halo exchange is in flight); the doubled
+            # ranks of the halo rows follow once it lands (run_step)
+            be.cs_rank_winsor_zn(X, outs, rank2=rk, dates=zd)
+            if rk is not None:
+                side["rank2_halo"] = (0, zd[0])
+        else:
+            be.cs_rank_winsor_zn(X, outs, rank2=rk)
         if side is not None:
             side["stats"] = None
             side["zscore"] = outs[2]                # the Gram's z (valid until the buffer is reused)
@@ -591,12 +603,15 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     side = {"rank2_buf": getattr(sp, "rank2", None), "R": sp.R, "lags": tuple(cfg.ic_lags)}
     streams = None
     early = not cfg.streams
-    # the four cross-sectional operators in one pass only without date shards: that pass also
-    # ranks the halo rows, which the first owned dates' daily IC reads (exposure date = target
-    # date - lag), so sharded it would have to wait for the halo exchange; the two-pass form
-    # keeps cs_zscore + neutralize and the Gram in front of the exchange (§7), which costs
-    # less per shard than an exposed exchange
-    zn = sp.world == 1
+    # the four cross-sectional operators in one pass.  Sharded, the pass runs on the owned
+    # dates while the halo exchange is in flight (every output row is per-date), and the
+    # doubled ranks of the halo rows -- the first owned dates' daily IC reads exposures at
+    # t - lag -- follow once the exchange lands (fmx_cs_rank2_dates).  A backend without
+    # date ranges takes the two-pass form sharded (cs_zscore + neutralize in front of the
+    # exchange, rank + winsor after it)
+    zn = sp.halo == 0 or (getattr(be, "zn_dates", False) and sp.X.shape[2] <= getattr(be, "ranked_ic_max_a", 0))
+    if zn and sp.halo > 0:
+        side["zn_dates"] = (sp.halo, sp.X.shape[1])
     early_names = EARLY_STAGES
     t0 = _ev(timers)
     halo = sp.exchange_halo_start()
@@ -617,6 +632,10 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     t0 = _ev(timers)
     sp.exchange_halo_finish(halo)
     _rec(timers, "halo_wait", t0)
+    if side.get("rank2_halo") is not None:
+        t0 = _ev(timers)
+        be.cs_rank2(sp.X, side["rank2"], dates=side.pop("rank2_halo"))
+        _rec(timers, "rank2_halo", t0)
     if cfg.streams and cfg.ops and hasattr(be, "ts_set") and sp.X.is_cuda:
         # fork: the rolling set and the cs_zscore -> Gram chain on side streams, the rank
         # pass -> IC -> selection chain on the current one; joined before the Gram sum

@@ -205,6 +205,17 @@ int64_t fmx_group_rank_sorted_work_bytes(int64_t F, int64_t D, int64_t A);
  * operator output of the same rows is wanted (factor_selector.py:36-48's rankdata). */
 fmx_status fmx_cs_rank2(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
                         void* stream);
+/* fmx_cs_rank_winsor_zn / fmx_cs_rank2 on the rows of dates [d0, d1) of every factor of an
+ * [F][D][ld] panel (outputs at the same rows; other rows untouched).  The date-sharded step
+ * runs the four operators on its owned dates while the halo exchange is in flight and the
+ * doubled ranks of the halo rows after it (the daily IC reads exposures at t - lag).
+ * Replaces the same reference functions as the two whole-panel entries
+ * (operations.py:54-68, :77-78, :171-182; factor_selector.py:36-48).  A <= 16384. */
+fmx_status fmx_cs_rank_winsor_zn_dates(const double* X, double* Yrank, double* Ywinsor, double* Yzscore,
+                                       double* Yneutralize, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t d0,
+                                       int64_t d1, double qlo, double qhi, fmx_rank2_t* rank2, void* stream);
+fmx_status fmx_cs_rank2_dates(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A, int64_t ld,
+                              int64_t d0, int64_t d1, void* stream);
 /* cs_winsor (operations.py:64-68); qlo/qhi are the fractions numpy sees
  * (pandas passes q*100 and numpy divides by 100). */
 fmx_status fmx_cs_winsor(const double* X, double* Y, int64_t F, int64_t D, int64_t A, int64_t ld, double qlo,

@@ -400,3 +400,28 @@ def test_gram_from_zscore_equals_gram_from_stats(dev, A):
     G2, N2 = E.gram_fused(Yz, None, 0, 12)
     assert np.array_equal(N1.cpu().numpy(), N2.cpu().numpy())
     assert np.array_equal(G1.cpu().numpy(), G2.cpu().numpy())
+
+
+@pytest.mark.parametrize("D,A,d0,d1", [(40, 700, 11, 29), (33, 5000, 21, 33), (25, 129, 0, 7), (30, 9000, 3, 30)])
+def test_date_range_entries_match_whole_panel_rows(dev, D, A, d0, d1):
+    """fmx_cs_rank_winsor_zn_dates / fmx_cs_rank2_dates (the sharded step: owned dates before
+    the halo lands, the halo rows' doubled ranks after): the rows of [d0, d1) bit-identical to
+    the whole-panel pass, every other row untouched."""
+    import torch
+    import factormodeling_amd.engine as E
+    X = torch.as_tensor(_panel(D * 7 + A, 3, D, A), device=dev)
+    rk_full = torch.empty(X.shape, dtype=E.RANK2_DTYPE, device=dev)
+    full = E.cs_rank_winsor_zn(X, rank2=rk_full)
+    outs = [torch.full_like(X, 7.0) for _ in range(4)]
+    rk = torch.full(X.shape, 12345, dtype=E.RANK2_DTYPE, device=dev)
+    E.cs_rank_winsor_zn(X, 0.01, 0.99, *outs, rank2=rk, dates=(d0, d1))
+    for got, ref in zip(outs, full):
+        g, r = got.cpu().numpy(), ref.cpu().numpy()
+        assert np.array_equal(g[:, d0:d1], r[:, d0:d1], equal_nan=True)
+        assert (g[:, :d0] == 7.0).all() and (g[:, d1:] == 7.0).all()
+    assert torch.equal(rk[:, d0:d1], rk_full[:, d0:d1])
+    assert (rk[:, :d0] == 12345).all() and (rk[:, d1:] == 12345).all()
+    # the halo rows' doubled ranks afterwards complete the panel
+    E.cs_rank2(X, rk, dates=(0, d0))
+    E.cs_rank2(X, rk, dates=(d1, D))
+    assert torch.equal(rk, rk_full)
