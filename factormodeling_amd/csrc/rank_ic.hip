@@ -104,7 +104,7 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
           const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
   // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64);
   // T[b] = start | end << 16 of its E entries in eb) and the entries eb[ICW_EC] grouped by
-  // block.  Dynamic LDS: ICW_WAVES * 2 * (nbp + ICW_EC) words.
+  // block.  Dynamic LDS: ICW_WAVES * 2 * (nbp + ICW_EC) + 2 words.
   extern __shared__ uint32_t icw_lds[];
   __shared__ double scr[ICW_WAVES * 32];
   // the wave index as a scalar: the row, its pointers and lags live in SGPRs (saddr loads)
@@ -281,9 +281,15 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     int corr = 0;
     if (ne[m]) {                              // wave-uniform
       const uint32_t tb = T[m][rk >> 6];
-      const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16;
+      const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16, nj = j1 - j0;
       corr = 2 * (int)j0;
-      for (uint32_t j = j0; j < j1; ++j) {    // this block's entries (usually none)
+      // the block's first two entries without a loop: with ~1 NaN return per 6 rank blocks
+      // nearly every wave has a lane whose block holds one, and a loop there made the whole
+      // wave run it (read past the list end: masked, and the LDS region is padded by 2)
+      const uint32_t e0 = eb[m][j0], e1 = eb[m][j0 + 1];
+      corr += nj > 0 ? (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) : 0;
+      corr += nj > 1 ? (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0) : 0;
+      for (uint32_t j = j0 + 2; j < j1; ++j) {   // a third entry or more (rare)
         const uint32_t e = eb[m][j];
         corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
       }
@@ -422,7 +428,7 @@ fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R,
     FMX_LAUNCH_CHECK("k_ic_empty");
     FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
     const int nbp = ((int)((2 * A) >> 6) + 2) & ~1;
-    const size_t lds = sizeof(uint32_t) * ICW_WAVES * 2 * (size_t)(nbp + ICW_EC);
+    const size_t lds = sizeof(uint32_t) * (ICW_WAVES * 2 * (size_t)(nbp + ICW_EC) + 2);   // + 2: k_ic_wave's e1 read
     k_ic_wave<<<wave_grid, 64 * ICW_WAVES, lds, st>>>(X, RK, R, F, D, A, ld, L0, L1, NL, o, pos, npos, ovf);
     FMX_LAUNCH_CHECK("k_ic_wave");
     void* args[] = {(void*)&X, (void*)&RK, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,
