@@ -272,29 +272,31 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     }
     if (i0 + 64 * ICW_PF < An) load(i0 + 64 * ICW_PF, ICW_PF - 1);
   };
-  auto accum = [&](int m, bool p, uint64_t bp, double x, uint32_t rk, double r) {
+  // the pair rank 2k = RK minus the E correction of lag m.  Branch-free for both lags (T is
+  // zeroed, so a lag without E entries reads j0 = j1 = 0): the two lags' table reads issue
+  // back to back and share one LDS latency.  The block's first two entries without a loop:
+  // with ~1 NaN return per 6 rank blocks nearly every wave has a lane whose block holds
+  // one, and a loop there made the whole wave run it (7.75 -> 7.30 ms at C2; a read past the
+  // list end is masked, and the LDS region is padded by 2)
+  auto pair_rank = [&](int m, uint32_t rk) {
+    const uint32_t tb = T[m][rk >> 6];
+    const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16, nj = j1 - j0;
+    int corr = 2 * (int)j0;
+    const uint32_t e0 = eb[m][j0], e1 = eb[m][j0 + 1];
+    corr += nj > 0 ? (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) : 0;
+    corr += nj > 1 ? (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0) : 0;
+    for (uint32_t j = j0 + 2; j < j1; ++j) {   // a third entry or more (rare)
+      const uint32_t e = eb[m][j];
+      corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
+    }
+    return rk - (uint32_t)corr;
+  };
+  auto accum = [&](int m, bool p, uint64_t bp, double x, uint32_t k2, double r) {
     // difference flags as wave masks: compares straight into scalar masks, ANDed with the
     // pair mask bp (a short-circuit p && ... would materialise the booleans in VGPRs)
     dm[2 * m] |= bp & __ballot(x != ax[m]);
     dm[2 * m + 1] |= bp & __ballot(r != ar[m]);
     if (!p) return;
-    int corr = 0;
-    if (ne[m]) {                              // wave-uniform
-      const uint32_t tb = T[m][rk >> 6];
-      const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16, nj = j1 - j0;
-      corr = 2 * (int)j0;
-      // the block's first two entries without a loop: with ~1 NaN return per 6 rank blocks
-      // nearly every wave has a lane whose block holds one, and a loop there made the whole
-      // wave run it (read past the list end: masked, and the LDS region is padded by 2)
-      const uint32_t e0 = eb[m][j0], e1 = eb[m][j0 + 1];
-      corr += nj > 0 ? (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) : 0;
-      corr += nj > 1 ? (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0) : 0;
-      for (uint32_t j = j0 + 2; j < j1; ++j) {   // a third entry or more (rare)
-        const uint32_t e = eb[m][j];
-        corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);
-      }
-    }
-    const uint32_t k2 = rk - (uint32_t)corr;
     const double dx = x - ax[m], dy = r - ar[m];
     // the moment sums with fused multiply-adds: the records are tolerance-pinned (single-pass
     // moments about the first pair, ~1e-15 relative), not bit-pinned, and an fma per term is
@@ -314,6 +316,7 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     double x, r[2];
     uint32_t rk;
     next(i0, x, rk, r);
+    const uint32_t k2[2] = {pair_rank(0, rk), pair_rank(1, rk)};
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const bool p = (x == x) & (r[m] == r[m]);
@@ -325,20 +328,21 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
         ar[m] = fr_readlane_d(r[m], l);
         ref[m] = true;
       }
-      if (ref[m]) accum(m, p, bp, x, rk, r[m]);   // before the shift: no pairs to add
+      if (ref[m]) accum(m, p, bp, x, k2[m], r[m]);   // before the shift: no pairs to add
     }
   }
   for (; i0 < An; i0 += 64) {
     double x, r[2];
     uint32_t rk;
     next(i0, x, rk, r);
+    const uint32_t k2[2] = {pair_rank(0, rk), pair_rank(1, rk)};
     const bool xo = x == x;
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const bool p = xo & (r[m] == r[m]);
       const uint64_t bp = __ballot(p);
       cnt[m] += __popcll(bp);
-      accum(m, p, bp, x, rk, r[m]);
+      accum(m, p, bp, x, k2[m], r[m]);
     }
   }
   // 3. butterflies into the wave's scratch: [0,6) lag 0's sums, [6,12) lag 1's, [12,14) the
