@@ -21,32 +21,79 @@ import torch
 import torch.distributed as dist
 
 
+class _HostRecv:
+    """A receive staged through host memory: wait() copies it into the device tensor."""
+
+    def __init__(self, req, host, out):
+        self.req, self.host, self.out = req, host, out
+
+    def wait(self):
+        self.req.wait()
+        self.out.copy_(self.host)
+
+
 class TorchComm:
-    """torch.distributed on the default process group (RCCL / gloo)."""
+    """torch.distributed on the default process group (RCCL / gloo).  RCCL orders its
+    transfers after the producing kernels of the current stream (and the current stream
+    after the received data on wait()).  gloo does not order its point-to-point transfers of
+    device tensors with the stream that produced them (a halo slab could be sent before
+    torch.cat had written it: seen as a wrong halo at world 3 on one GPU), so with gloo every
+    device tensor is staged through host memory: sends copy it out (stream-synchronous),
+    receives land in host buffers copied in on wait(), collectives run on host copies."""
 
     def __init__(self):
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
+        self.host_staged = dist.get_backend() == "gloo"
+
+    def _stage(self, t):
+        return t.cpu() if self.host_staged and t.is_cuda else t
 
     def isend(self, t, dst):
-        return dist.isend(t, dst)
+        return dist.isend(self._stage(t), dst)
 
     def irecv(self, t, src):
+        if self.host_staged and t.is_cuda:
+            host = torch.empty(t.shape, dtype=t.dtype)
+            return _HostRecv(dist.irecv(host, src), host, t)
         return dist.irecv(t, src)
 
     def exchange(self, sends, recvs):
         """Point-to-point sends [(t, dst)] and receives [(t, src)] posted as ONE
         ``batch_isend_irecv`` group (RCCL coalesces the group's transfers); the returned
         requests are waited on by the caller."""
-        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends] + [dist.P2POp(dist.irecv, t, s) for t, s in recvs]
-        return dist.batch_isend_irecv(ops) if ops else []
+        ops, outs = [], []
+        for t, d in sends:
+            ops.append(dist.P2POp(dist.isend, self._stage(t), d))
+        for t, s in recvs:
+            if self.host_staged and t.is_cuda:
+                host = torch.empty(t.shape, dtype=t.dtype)
+                ops.append(dist.P2POp(dist.irecv, host, s))
+                outs.append((host, t))
+            else:
+                ops.append(dist.P2POp(dist.irecv, t, s))
+                outs.append(None)
+        if not ops:
+            return []
+        reqs = dist.batch_isend_irecv(ops)
+        nsend = len(sends)
+        res = list(reqs[:nsend])
+        for r, o in zip(reqs[nsend:], outs):
+            res.append(_HostRecv(r, *o) if o is not None else r)
+        return res
 
     def all_gather(self, t):
-        parts = [torch.empty_like(t) for _ in range(self.world)]
-        dist.all_gather(parts, t.contiguous())
-        return parts
+        src = self._stage(t.contiguous())
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src)
+        return [p.to(t.device) for p in parts] if src is not t and t.is_cuda else parts
 
     def all_reduce_sum(self, t):
+        if self.host_staged and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
