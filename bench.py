@@ -294,8 +294,17 @@ def main():
                "host_cpus": ncpu, "cpu_model": model}
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one GPU per rank; FMX_BENCH_DIST_BACKEND=gloo (tests only) runs the same multi-rank
+        # bench over gloo with the ranks sharing the visible devices (RCCL refuses two ranks
+        # on one device)
+        backend = os.environ.get("FMX_BENCH_DIST_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     from factormodeling_amd import pipeline as PL
 

@@ -89,3 +89,24 @@ def test_torchcomm_multi_process_step_matches_one_shard(world):
             if ":" in k:                     # operator outputs on the owned dates
                 np.testing.assert_allclose(v, col1[k][:, lo:hi], rtol=1e-12, atol=1e-12, equal_nan=True,
                                            err_msg=f"{k} rank {rank}")
+
+
+@pytest.mark.timeout(400)
+def test_bench_multi_rank_over_gloo():
+    """bench.py's multi-rank path (its own rank launcher, barrier + max-over-ranks timing,
+    one JSON line from rank 0) with 2 ranks on the one GPU over gloo
+    (FMX_BENCH_DIST_BACKEND=gloo; the driver's multi-GPU run uses RCCL)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMX_BENCH_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup",
+                          "1", "--dates", "504", "--factors", "20"], env=env, capture_output=True, text=True,
+                         timeout=360)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "date-shard2"
+    assert line["value"] > 0 and line["unit"] == "factor·asset·days/s"
+    assert line["value"] == pytest.approx(504 * 5000 * 20 / (line["ms_per_step"] * 1e-3), rel=1e-6)
