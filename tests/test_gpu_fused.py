@@ -402,7 +402,8 @@ def test_gram_from_zscore_equals_gram_from_stats(dev, A):
     assert np.array_equal(G1.cpu().numpy(), G2.cpu().numpy())
 
 
-@pytest.mark.parametrize("D,A,d0,d1", [(40, 700, 11, 29), (33, 5000, 21, 33), (25, 129, 0, 7), (30, 9000, 3, 30)])
+@pytest.mark.parametrize("D,A,d0,d1", [(40, 700, 11, 29), (33, 5000, 21, 33), (25, 129, 0, 7), (30, 9000, 3, 30),
+                                         (20, 10000, 5, 17)])
 def test_date_range_entries_match_whole_panel_rows(dev, D, A, d0, d1):
     """fmx_cs_rank_winsor_zn_dates / fmx_cs_rank2_dates (the sharded step: owned dates before
     the halo lands, the halo rows' doubled ranks after): the rows of [d0, d1) bit-identical to
