@@ -128,7 +128,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    p.add_argument("--workload", choices=["c2", "c4", "c5", "c1-dropin", "c2-dropin-slice"], default="c2")
     p.add_argument("--dates", type=int, default=None)
     p.add_argument("--assets", type=int, default=None)
     p.add_argument("--factors", type=int, default=None)
@@ -147,7 +147,9 @@ def _port_worker(args):
     D, A, seed, ic_dates = args
     sys.path.insert(0, ROOT)
     import oracle.metrics as OM
+    import oracle.numerics as nm
     import oracle.ops as O
+    nm.FAST = True                 # 1-D pairwise sums by numpy's add.reduce (the same algorithm)
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((D, A))
     x = np.where(rng.random((D, A)) < 0.05, np.round(x, 1), x)
@@ -172,13 +174,16 @@ def cpu_baseline(D, A, workers=16, ic_dates=126):
     window metrics + icir_top selection over all processed days and the factor Gram of the
     sampled factors.  Must run before this process touches the GPU (children are spawned).
     Returns (factor·asset·days/s, cores, description)."""
+    import oracle.numerics as nm
+    nm.FAST = True                 # numpy's own add.reduce for 1-D pairwise sums
     import concurrent.futures as cf
     import multiprocessing as mp
     import oracle.gram as OG
     import oracle.metrics as OM
     Fs = workers
     t0 = time.perf_counter()
-    with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+    with _single_thread_children(), cf.ProcessPoolExecutor(max_workers=workers,
+                                                           mp_context=mp.get_context("spawn")) as ex:
         res = list(ex.map(_port_worker, [(D, A, 1000 + f, ic_dates) for f in range(Fs)]))
     t_spawned = time.perf_counter() - t0
     # per-worker wall = ops + scaled IC; the concurrent run lasts as long as the slowest
@@ -207,6 +212,140 @@ def cpu_baseline(D, A, workers=16, ic_dates=126):
             f"(slowest worker {t_par:.1f}s), window metrics + icir_top for {D - W - 1} days ({t_sel:.1f}s), "
             f"factor Gram ({Dg} dates measured, scaled: {t_gram:.1f}s); measured wall incl. process start "
             f"{t_spawned:.1f}s")
+    return units / wall, workers, desc
+
+
+class _single_thread_children:
+    """Spawned port workers run single-threaded BLAS (one core each): without this every
+    worker's numpy starts a full thread pool and 16 workers oversubscribe the host."""
+    KEYS = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.KEYS}
+        for k in self.KEYS:
+            os.environ[k] = "1"
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _port_worker_wide(args):
+    """One factor of the C4 / C5 step on the numpy oracle port (child process, no GPU).
+    c4: daily IC lag 1 on ``ic_dates`` dates (scaled to D).  c5: the feature
+    sign(ts_corr(x, R, 60)) * x / ts_std(x, 60) over ``feat_dates`` dates (scaled), then its
+    daily IC lags 1-2 on ``ic_dates`` dates (scaled).  Returns the factor's scaled seconds."""
+    wl, D, A, seed, ic_dates, feat_dates = args
+    sys.path.insert(0, ROOT)
+    import oracle.metrics as OM
+    import oracle.numerics as nm
+    import oracle.ops as O
+    nm.FAST = True                 # 1-D pairwise sums by numpy's add.reduce (the same algorithm)
+    rng = np.random.default_rng(seed)
+    Dm = min(D, max(ic_dates, feat_dates) + 2)
+    x = rng.standard_normal((Dm, A))
+    x = np.where(rng.random((Dm, A)) < 0.05, np.round(x, 1), x)
+    x[rng.random(x.shape) < 0.01] = np.nan
+    r = 0.01 * rng.standard_normal((Dm, A))
+    t = 0.0
+    lags = (1,)
+    if wl == "c5":
+        Df = min(Dm, feat_dates)
+        t0 = time.perf_counter()
+        x = O.corr_vol_feature(x[:Df], r[:Df], 60)
+        t += (time.perf_counter() - t0) * (D / Df)
+        x = np.where(np.isnan(x), rng.standard_normal(x.shape), x)    # past the warm-up: all-valid rows
+        lags = (1, 2)
+    Di = min(x.shape[0], ic_dates)
+    t0 = time.perf_counter()
+    for d in range(2, Di):
+        for L in lags:
+            OM.daily_stats(x[d - L], r[d])
+    t += (time.perf_counter() - t0) * (D / (Di - 2))
+    return t
+
+
+def cpu_baseline_wide(wl, D, A, F, workers=16, ic_dates=64, feat_dates=504):
+    """The numpy oracle PORT of the C4 / C5 step: per-factor work on
+    ``workers`` host processes (one factor each, concurrent: the slowest worker's time x
+    F / workers factors per worker), then the whole-zoo stages measured on samples and scaled
+    -- C4: the full-sample metrics (summarize) of every factor, the 2000 x 2000 Gram (the
+    z-score pass scaled by F·D·A, the Z^T Z product by F^2·D·A flops; numpy BLAS) and the
+    greedy prune; C5: window metrics + icir_top for every processed day (scaled by F) and
+    the weighted composite of every processed day (sampled days, scaled).  Must run before
+    this process touches the GPU.  Returns (factor·asset·days/s, cores, description)."""
+    import oracle.numerics as nm
+    nm.FAST = True                 # numpy's own add.reduce for 1-D pairwise sums
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import oracle.gram as OG
+    import oracle.metrics as OM
+    Fs = workers
+    t0 = time.perf_counter()
+    with _single_thread_children(), cf.ProcessPoolExecutor(max_workers=workers,
+                                                           mp_context=mp.get_context("spawn")) as ex:
+        res = list(ex.map(_port_worker_wide, [(wl, D, A, 1000 + f, ic_dates, feat_dates) for f in range(Fs)]))
+    t_spawned = time.perf_counter() - t0
+    t_par = max(res) * (F / workers)
+    rng = np.random.default_rng(7)
+    parts = [f"per-factor work on {workers} processes: slowest factor {max(res):.2f}s x {F}/{workers} "
+             f"factors per process = {t_par:.1f}s"]
+    if wl == "c4":
+        daily = rng.standard_normal((4, Fs, D)) * 0.05
+        t0 = time.perf_counter()
+        for f in range(Fs):
+            OM.summarize(daily[1, f], daily[2, f], daily[3, f])
+        t_sum = (time.perf_counter() - t0) * (F / Fs)
+        Fg, Dg = 256, 16
+        Xg = rng.standard_normal((Fg, Dg, A))
+        t0 = time.perf_counter()
+        Z, M = OG.zscore_exposures(Xg)
+        t_z = (time.perf_counter() - t0) * (F * D) / (Fg * Dg)
+        Zf, Mf = Z.reshape(Fg, -1), M.reshape(Fg, -1)
+        t0 = time.perf_counter()
+        Zf @ Zf.T
+        Mf @ Mf.T
+        t_mm = (time.perf_counter() - t0) * (F / Fg) ** 2 * (D / Dg)
+        Cg = np.corrcoef(rng.standard_normal((F, 64)))
+        t0 = time.perf_counter()
+        OG.greedy_prune(Cg, list(range(F)), 0.7, None)
+        t_pr = time.perf_counter() - t0
+        wall = t_par + t_sum + t_z + t_mm + t_pr
+        parts.append(f"full-sample metrics {t_sum:.2f}s; Gram: z pass {t_z:.1f}s ({Fg}x{Dg}x{A} measured, scaled "
+                     f"by F·D), Z^T Z + M^T M {t_mm:.1f}s ({Fg}x{Fg} over {Dg} dates measured, scaled by F^2·D); "
+                     f"greedy prune {t_pr:.2f}s")
+    else:
+        W = 60
+        daily = rng.standard_normal((4, Fs, D)) * 0.05
+        t0 = time.perf_counter()
+        J = D - W - 1
+        Js = 200
+        for i in range(W, W + Js):
+            vals = np.array([OM.summarize(daily[1, f, i - W + 1:i], daily[2, f, i - W + 1:i],
+                                          daily[3, f, i - W + 1:i]) for f in range(Fs)])
+            OM.icir_top(OM.nargsort_desc(vals[:, 3]), vals, -1.0, 5)
+        t_sel = (time.perf_counter() - t0) * (F / Fs) * (J / Js)
+        import oracle.composite as OC
+        from factormodeling_amd.pipeline import factor_names
+        names = factor_names(F)
+        nd = 8
+        Xd = rng.standard_normal((F, nd, A))
+        Wd = np.zeros((nd, F))
+        for i in range(nd):
+            Wd[i, rng.choice(F, 5, replace=False)] = 0.2
+        t0 = time.perf_counter()
+        OC.weighted_composite_factor(Xd, names, list(range(nd)), Wd, "zscore")
+        t_comp = (time.perf_counter() - t0) * (J / nd)
+        wall = t_par + t_sel + t_comp
+        parts.append(f"window metrics + icir_top for {J} days ({Js} days x {Fs} factors measured, scaled: "
+                     f"{t_sel:.1f}s); weighted composite ({nd} days measured, scaled: {t_comp:.1f}s)")
+    units = float(F) * D * A
+    desc = (f"numpy oracle port of {wl.upper()} ({F} factors x {D} dates x {A} assets): " + "; ".join(parts) +
+            f"; per-factor samples: {ic_dates} IC dates" + (f", {feat_dates} feature dates" if wl == "c5" else "") +
+            f"; measured wall incl. process start {t_spawned:.1f}s")
     return units / wall, workers, desc
 
 
@@ -260,8 +399,101 @@ def spawn_ranks(n):
     return bad[0] if bad else 0
 
 
+# the reference's own timings of the same calls (build container, 1 core)
+DROPIN_REFERENCE_S = {
+    "c1-dropin": {"cs_rank": 0.73, "cs_zscore": 0.52, "ts_mean(20)": 0.73, "ts_std(20)": 0.87,
+                  "single_factor_metrics": 5.00, "FactorSelector(icir_top,60).prepare_selection": 292.2,
+                  "weighted_composite_factor(zscore)": 7.34, "total": 307.4},
+    # config-2 slices (2520 x 5000 x 2; single_factor_metrics measured at 200 dates, the
+    # FactorSelector at 0.234 s per processed day): scaled to the slice's 2520 dates
+    "c2-dropin-slice": {"cs_rank": 3.11, "cs_zscore": 2.94, "ts_mean(20)": 3.82, "ts_std(20)": 4.10,
+                        "single_factor_metrics": 1.33 * 2520 / 200,
+                        "FactorSelector(icir_top,60).prepare_selection": 0.234 * (2520 - 61)},
+}
+
+
+def dropin_bench(args):
+    """The drop-in API end to end: the calls pipeline.ipynb makes
+    (:216 single_factor_metrics, :351-361 FactorSelector(icir_top, window=60).prepare_selection,
+    :461-463 weighted_composite_factor, plus the C1 operators) on pandas MultiIndex input, with
+    the host <-> device boundary broken out (factormodeling_amd.profiling: pandas -> dense,
+    H2D, D2H, dense -> pandas, host planning; the rest of each call's wall time is the device
+    work -- launches and kernels -- and Python glue).  Not the driver's line."""
+    import pandas as pd
+    from factormodeling_amd import profiling
+    from factormodeling_amd.dropin import composite_factor as cf
+    from factormodeling_amd.dropin import factor_selector as fsel
+    from factormodeling_amd.dropin import operations as ops
+    D, A, F = (500, 1000, 20) if args.workload == "c1-dropin" else (2520, 5000, 2)
+    D, A, F = args.dates or D, args.assets or A, args.factors or F
+    rng = np.random.default_rng(0)
+    names = [f"g{k // 4:03d}_{k:04d}_{['eq', 'flx', 'long', 'short', 'raw'][k % 5]}" for k in range(F)]
+    X = rng.standard_normal((D, A, F))
+    tie = rng.random(X.shape) < 0.05
+    X[tie] = np.round(X[tie], 1)
+    X[rng.random(X.shape) < 0.01] = np.nan
+    r = 0.01 * rng.standard_normal((D, A))
+    r[1:] += 0.002 * np.nan_to_num(X[:-1, :, 0])
+    r[rng.random((D, A)) < 0.005] = np.nan
+    dates = pd.bdate_range("2015-01-01", periods=D)
+    idx = pd.MultiIndex.from_product([dates, [f"S{i:05d}" for i in range(A)]], names=["date", "symbol"])
+    df = pd.DataFrame(X.reshape(D * A, F), index=idx, columns=names)
+    ret = pd.Series(r.reshape(-1), index=idx, name="log_return")
+    fret = pd.DataFrame(0.01 * rng.standard_normal((D, F)), index=pd.Index(dates, name="date"), columns=names)
+    state = {}
+
+    def sel_call():
+        state["sel"] = fsel.FactorSelector(df, ret, fret, window=60, method="icir_top",
+                                           method_kwargs={"top_x": 5, "icir_threshold": -1}).prepare_selection()
+        return state["sel"]
+
+    calls = [("cs_rank", lambda: ops.cs_rank(df)), ("cs_zscore", lambda: ops.cs_zscore(df)),
+             ("ts_mean(20)", lambda: ops.ts_mean(df, 20)), ("ts_std(20)", lambda: ops.ts_std(df, 20)),
+             ("single_factor_metrics", lambda: fsel.single_factor_metrics(df, ret)),
+             ("FactorSelector(icir_top,60).prepare_selection", sel_call),
+             ("weighted_composite_factor(zscore)", lambda: cf.weighted_composite_factor(df, state["sel"], "zscore"))]
+    out = {}
+    for name, fn in calls:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()                                   # cold: first call (index build, library / schedule setup)
+        torch.cuda.synchronize()
+        cold = time.perf_counter() - t0
+        walls, phs = [], []
+        for _ in range(max(1, args.steps)):
+            with profiling.record() as ph:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                walls.append(time.perf_counter() - t0)
+            phs.append(dict(ph))
+        k = int(np.argsort(walls)[len(walls) // 2])
+        wall, ph = walls[k], phs[k]
+        rec = {"wall_s": wall, "cold_s": cold}
+        rec.update({f"{p}_s": v for p, v in sorted(ph.items())})
+        rec["device_and_glue_s"] = wall - sum(ph.values())
+        ref = DROPIN_REFERENCE_S.get(args.workload, {}).get(name)
+        if ref is not None:
+            rec["reference_s"] = ref
+            rec["speedup_vs_reference"] = ref / wall
+        out[name] = rec
+    tot = sum(v["wall_s"] for v in out.values())
+    ref_tot = DROPIN_REFERENCE_S.get(args.workload, {}).get("total")
+    line = {"metric": "drop-in API wall time (pandas in, pandas out)", "value": tot, "unit": "s",
+            "higher_is_better": False, "n_gpus": 1, "steps": args.steps, "dtype": "f64",
+            "data": "synthetic (SURVEY 8(d) generator, host numpy -> pandas MultiIndex)",
+            "config": {"workload": args.workload, "dates": D, "assets": A, "factors": F},
+            "calls": out, "reference_total_s": ref_tot,
+            "speedup_vs_reference": (ref_tot / tot) if ref_tot else None,
+            "reference_source": "SURVEY.md §6 (the reference itself, 1 core, build container)"}
+    print(json.dumps(line))
+
+
 def main():
     args = parse()
+    if args.workload in ("c1-dropin", "c2-dropin-slice"):
+        return dropin_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -283,10 +515,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before this process initialises the GPU: the port's workers are spawned children
         dims0 = WORKLOAD_DIMS[args.workload]
-        rate, cores, sample = cpu_baseline(args.dates or dims0[0], args.assets or dims0[1], args.cpu_workers)
+        Db, Ab, Fb = args.dates or dims0[0], args.assets or dims0[1], args.factors or dims0[2]
+        if args.workload == "c2":
+            rate, cores, sample = cpu_baseline(Db, Ab, args.cpu_workers)
+        else:
+            rate, cores, sample = cpu_baseline_wide(args.workload, Db, Ab, Fb, args.cpu_workers)
         ncpu, model = host_cpu()
         # cores: the worker processes the port actually used (one thread each); host_cpus:
         # the logical CPUs of the machine (the GPU box exposes many more than its CPU share)

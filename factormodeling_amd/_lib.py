@@ -22,6 +22,7 @@ c_i32, c_i64, c_dbl, c_vp, c_cp = ctypes.c_int32, ctypes.c_int64, ctypes.c_doubl
 SIGNATURES = {
     "fmx_last_error": [],
     "fmx_abi_version": [],
+    "fmx_build_variant": [],
     "fmx_device_info": [c_cp, c_i64],
     "fmx_ts_op": [c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp],
     "fmx_ts_set": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp],
@@ -97,7 +98,7 @@ SIGNATURES = {
     "fmx_daily_corr": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp],
     "fmx_wcomp_combine": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"fmx_last_error": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64, "fmx_gram_direct_work_bytes": c_i64,
+_RESTYPES = {"fmx_last_error": c_cp, "fmx_build_variant": c_cp, "fmx_ic_ranked_work_len": c_i64, "fmx_rank_ic_work_len": c_i64, "fmx_gram_work_bytes": c_i64, "fmx_gram_direct_work_bytes": c_i64,
              "fmx_gram_direct_exact_work_bytes": c_i64, "fmx_ic_daily_sorted_work_bytes": c_i64,
              "fmx_group_op_long_work_bytes": c_i64,
              "fmx_gram_fused_work_bytes": c_i64, "fmx_corr_prune_windows_work_bytes": c_i64,
@@ -136,6 +137,10 @@ def load(path: str = None):
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, c_i32)
+        variant = lib.fmx_build_variant().decode()
+        if variant != "product" and os.environ.get("FMX_ALLOW_DIAG") != "1":
+            raise FmxError(f"{p} is a {variant} build (wrong-result timing arms); "
+                           f"set FMX_ALLOW_DIAG=1 to load it for A/B timing")
         if path is None:
             _lib = lib
         return lib

@@ -39,7 +39,12 @@ class TorchComm:
     device tensors with the stream that produced them (a halo slab could be sent before
     torch.cat had written it: seen as a wrong halo at world 3 on one GPU), so with gloo every
     device tensor is staged through host memory: sends copy it out (stream-synchronous),
-    receives land in host buffers copied in on wait(), collectives run on host copies."""
+    receives land in host buffers copied in on wait(), collectives run on host copies.
+
+    Consequence for timing: under gloo the staging copy blocks until the stream
+    drains, so the halo exchange is synchronous and never overlaps the owned-date fused pass
+    the step posts behind it -- gloo runs check correctness, not overlap.  Only the nccl
+    (RCCL) backend, i.e. the driver's multi-GPU bench, exercises the overlapped ordering."""
 
     def __init__(self):
         self.rank = dist.get_rank()

@@ -18,6 +18,7 @@ import torch
 
 from . import engine
 from .panel import device, panel_index
+from .profiling import phase
 
 
 def _prefix_groups(names):
@@ -129,9 +130,14 @@ def weighted_composite_factor(factors_df: pd.DataFrame, selection_df: pd.DataFra
     used = [c for c in selection_df.columns if (selection_df[c] > 0).any()]
     P = panel_index(factors_df.index)
     dev = device()
-    X = P.to_device(factors_df[used].to_numpy(dtype=np.float64, na_value=np.nan), dev) if used else \
-        torch.zeros((1, P.D, P.A), dtype=torch.float64, device=dev)
-    plan = _weighted_plan(P, selection_df, used)
+    if used:
+        with phase("pandas->dense"):
+            xv = factors_df[used].to_numpy(dtype=np.float64, na_value=np.nan)
+        X = P.to_device(xv, dev)
+    else:
+        X = torch.zeros((1, P.D, P.A), dtype=torch.float64, device=dev)
+    with phase("host plan"):
+        plan = _weighted_plan(P, selection_df, used)
     out = engine.wcomp(X, plan, method, P.present(dev))
     vals = P.from_device(out.unsqueeze(0))[:, 0]
     return pd.Series(vals, index=factors_df.index, name="composite_factor")

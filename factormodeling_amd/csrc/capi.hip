@@ -148,6 +148,19 @@ extern "C" const char* fmx_last_error(void) { return g_err.c_str(); }
 
 extern "C" int32_t fmx_abi_version(void) { return FMX_ABI_VERSION; }
 
+// Build variant: "product", or "diagnostic: <translation units>" when any unit was built
+// with -DFMX_DIAG (fmx_common.hpp) -- such a library computes wrong results on purpose.
+// (a function-local static: other units' load-time constructors may run before this one's)
+static std::string& build_variant() {
+  static std::string v = "product";
+  return v;
+}
+extern "C" void fmx_mark_diag(const char* tu) {
+  std::string& v = build_variant();
+  v = (v == "product" ? std::string("diagnostic:") : v + ",") + " " + tu;
+}
+extern "C" const char* fmx_build_variant(void) { return build_variant().c_str(); }
+
 extern "C" fmx_status fmx_device_info(char* buf, int64_t buflen) {
   FMX_ARG(buf && buflen > 0, "buffer");
   int dev = 0;

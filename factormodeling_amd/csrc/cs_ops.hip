@@ -991,8 +991,18 @@ extern "C" fmx_status fmx_cs_rank_winsor_zn_dates(const double* X, double* Yrank
   if (e) return e;
   e = br_cs_rank_winsor_zn(X, Yrank, Ywinsor, Yz, Yn, F, D, A, ld, d0, d1, qlo, qhi, rank2, pw, pw_len((int)A),
                            as_stream(stream));
-  if (e == FMX_ERR_UNSUPPORTED) set_error("fmx_cs_rank_winsor_zn_dates: rows of the fine-bucket kernel only");
-  return e;
+  if (e != FMX_ERR_UNSUPPORTED) return e;
+  // rows the fused kernel does not take (FMX_RANK_IMPL=br, or its LDS does not fit): the
+  // two-pass form of fmx_cs_rank_winsor_zn, one factor's date range [d0, d1) at a time (a
+  // [1][d1 - d0][ld] panel at row (f, d0)) -- as the whole-panel entry falls back
+  for (int64_t f = 0; f < F; ++f) {
+    const int64_t o = (f * D + d0) * ld;
+    fmx_rank2_t* rk = rank2 ? rank2 + o : nullptr;
+    if ((e = fmx_cs_rank_winsor(X + o, Yrank + o, Ywinsor + o, 1, d1 - d0, A, ld, qlo, qhi, nullptr, rk, stream)))
+      return e;
+    if ((e = fmx_cs_zscore_neutralize(X + o, Yz + o, Yn + o, 1, d1 - d0, A, ld, nullptr, nullptr, stream))) return e;
+  }
+  return FMX_OK;
 }
 
 extern "C" fmx_status fmx_cs_rank2_dates(const double* X, fmx_rank2_t* rank2, int64_t F, int64_t D, int64_t A,

@@ -14,6 +14,23 @@
 
 #define FMX_WAVE 64
 
+// Diagnostic (wrong-result) arms of the hot kernels exist for same-call A/B timing only
+// (FR_DIAG_*, GDB_DIAG_*, GW_DIAG).  Each needs -DFMX_DIAG as well, and a translation unit
+// built with FMX_DIAG registers itself at load time, so fmx_build_variant() names the
+// library "diagnostic" and the Python loader refuses it unless FMX_ALLOW_DIAG=1.
+#if !defined(FMX_DIAG) && (defined(FR_DIAG_NOZNSUM) || defined(FR_DIAG_NOSCAN) || defined(FR_DIAG_NOPF) ||      \
+                           defined(FR_DIAG_NOSTORE) || defined(GDB_DIAG_NOSTAGE) || (defined(GW_DIAG) && GW_DIAG != 0))
+#error "diagnostic kernel arms need -DFMX_DIAG (and the library then loads only with FMX_ALLOW_DIAG=1)"
+#endif
+extern "C" void fmx_mark_diag(const char* tu);
+#ifdef FMX_DIAG
+namespace {
+struct FmxDiagMark {
+  FmxDiagMark() { fmx_mark_diag(__FILE__); }
+} fmx_diag_mark_;
+}  // namespace
+#endif
+
 namespace fmx {
 
 void set_error(const std::string& msg);

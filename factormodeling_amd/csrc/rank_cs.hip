@@ -35,7 +35,7 @@ fmx_status br_cs_rank(const double* X, double* Y, int64_t F, int64_t D, int64_t 
                   (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * D == 0) return FMX_OK;
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(kfr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(set_dyn_lds(kfr, ll.bytes));
   FMX_HIP(hipLaunchKernel(kfr, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
@@ -59,7 +59,7 @@ fmx_status br_cs_rank_winsor(const double* X, double* Yr, double* Yw, int64_t F,
   int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(set_dyn_lds(k, ll.bytes));
   FMX_HIP(hipLaunchKernel(k, fmx_grid2(D, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }

@@ -36,7 +36,7 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
   int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(set_dyn_lds(k, ll.bytes));
   FMX_HIP(hipLaunchKernel(k, fmx_grid2(d1 - d0, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }
@@ -84,7 +84,7 @@ fmx_status br_cs_rank2(const double* X, fmx_rank2_t* RK, int64_t F, int64_t D, i
   int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Y, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Y2, (void*)&qlo, (void*)&qhi, (void*)&RK, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(set_dyn_lds(k, ll.bytes));
   FMX_HIP(hipLaunchKernel(k, fmx_grid2(d1 - d0, F), dim3(nt_fa), args, ll.bytes, st));
   return FMX_OK;
 }

@@ -528,7 +528,7 @@ fmx_status br_cs_rank_winsor_ic(const double* X, double* Yr, double* Yw, const d
   int lcap = ll.cap;
   void* args[] = {(void*)&X, (void*)&Yr, (void*)&D, (void*)&A, (void*)&ld, (void*)&method, (void*)&present,
                   (void*)&Yw, (void*)&qlo, (void*)&qhi, (void*)&RKrow, (void*)&ic, (void*)&zn, (void*)&lcap};
-  if (ll.bytes > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll.bytes));
+  FMX_HIP(set_dyn_lds(k, ll.bytes));
   FMX_HIP(hipLaunchKernel(k, fmx_grid2(F, D), dim3(nt_fa), args, ll.bytes, st));   // date-major rows
   static const int list_grid = [] {
     int dev = 0, cus = 0;

@@ -38,12 +38,39 @@ static inline int rank_impl() {
   return v;
 }
 
+// Static LDS bytes of kernel k, queried once per kernel (the hot rank launches ask on every
+// step; the answer never changes: ADVICE r5).  -1 when the query fails.
+static inline int64_t kern_static_lds(const void* k) {
+  static std::mutex mu;
+  static std::map<const void*, int64_t> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(k);
+  if (it != cache.end()) return it->second;
+  hipFuncAttributes at;
+  const int64_t v = hipFuncGetAttributes(&at, k) == hipSuccess ? (int64_t)at.sharedSizeBytes : -1;
+  cache.emplace(k, v);
+  return v;
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) above the 64 KiB default, once per
+// (kernel, size) high-water mark.
+static inline hipError_t set_dyn_lds(const void* k, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  static std::mutex mu;
+  static std::map<const void*, size_t> done;
+  std::lock_guard<std::mutex> g(mu);
+  size_t& d = done[k];
+  if (bytes <= d) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) d = bytes;
+  return e;
+}
+
 // True when kernel k (static LDS) plus dyn bytes of dynamic LDS fit one CU's 160 KiB.
 static inline bool lds_fits(const void* k, size_t dyn) {
   if (!k) return false;
-  hipFuncAttributes at;
-  if (hipFuncGetAttributes(&at, k) != hipSuccess) return false;
-  return at.sharedSizeBytes + dyn <= 160 * 1024;
+  const int64_t st = kern_static_lds(k);
+  return st >= 0 && (size_t)st + dyn <= 160 * 1024;
 }
 
 // Dynamic LDS of a fine-bucket rank launch with its in-bucket scan list (finerank.hpp
@@ -56,9 +83,8 @@ struct FrListLds {
   size_t bytes;
 };
 static inline FrListLds fr_list_lds(const void* k, int64_t A, size_t base, size_t extra) {
-  hipFuncAttributes at;
-  size_t stat = 0;
-  if (k && hipFuncGetAttributes(&at, k) == hipSuccess) stat = at.sharedSizeBytes;
+  const int64_t sl = k ? kern_static_lds(k) : -1;
+  const size_t stat = sl > 0 ? (size_t)sl : 0;
   // per-workgroup LDS is allocated in granules (2 KiB assumed: LDS_Block_Size reports
   // multiples of it), so the rows per CU are counted on rounded sizes
   const size_t cu = 160 * 1024, gran = 2048;
@@ -82,7 +108,7 @@ static inline fmx_status launch_br(K kern_table, int nt, int64_t A, int64_t inne
   if (!k) { set_error("row too long for the bucket-rank kernels (A > 16384)"); return FMX_ERR_UNSUPPORTED; }
   if (inner <= 0 || outer <= 0) return FMX_OK;
   if (inner * nt > 0xffffffffll || outer > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
-  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  FMX_HIP(set_dyn_lds(k, lds));
   FMX_HIP(hipLaunchKernel(k, fmx_grid2(inner, outer), dim3(nt), args, lds, st));
   return FMX_OK;
 }
@@ -93,7 +119,7 @@ static inline fmx_status launch_persistent(const void* k, int nt, int64_t nrows,
                                            hipStream_t st) {
   if (!k) { set_error("row too long for the fine-bucket kernels"); return FMX_ERR_UNSUPPORTED; }
   if (nrows <= 0) return FMX_OK;
-  if (lds > 64 * 1024) FMX_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  FMX_HIP(set_dyn_lds(k, lds));
   static std::mutex mu;
   static std::map<std::pair<const void*, size_t>, int64_t> cache;
   int64_t slots;

@@ -27,6 +27,7 @@ from . import engine
 from .factor_selection_methods import (corr_prune_selector, factor_momentum_selector, icir_top_selector,
                                        mvo_selector)
 from .panel import device, panel_index
+from .profiling import phase
 
 logger = logging.getLogger("factor_selector")
 
@@ -59,9 +60,12 @@ def _metrics_frame(vals: np.ndarray, names) -> pd.DataFrame:
 def _dense_inputs(factors_df: pd.DataFrame, returns: pd.Series):
     P = panel_index(factors_df.index)
     dev = device()
-    X = P.to_device(factors_df.to_numpy(dtype=np.float64, na_value=np.nan), dev)
-    r = returns if returns.index.equals(factors_df.index) else returns.reindex(factors_df.index)
-    R = P.to_device(r.to_numpy(dtype=np.float64, na_value=np.nan), dev)[0]
+    with phase("pandas->dense"):
+        xv = factors_df.to_numpy(dtype=np.float64, na_value=np.nan)
+        r = returns if returns.index.equals(factors_df.index) else returns.reindex(factors_df.index)
+        rv = r.to_numpy(dtype=np.float64, na_value=np.nan)
+    X = P.to_device(xv, dev)
+    R = P.to_device(rv, dev)[0]
     return P, X, R
 
 
@@ -80,8 +84,11 @@ def single_factor_metrics(factors_df: pd.DataFrame, returns: pd.Series) -> pd.Da
     names = [c for c in factors_df.columns]
     P, X, R = _dense_inputs(factors_df[names], returns)
     daily = _daily(P, X, R, 1)
-    summ = engine.ic_window(daily, [0], [P.D])[0].cpu().numpy()
-    return _metrics_frame(summ, names)
+    summ = engine.ic_window(daily, [0], [P.D])[0]
+    with phase("D2H"):
+        summ = summ.cpu().numpy()
+    with phase("dense->pandas"):
+        return _metrics_frame(summ, names)
 
 
 class FactorSelector:
@@ -178,10 +185,13 @@ class FactorSelector:
                 w = engine.corr_prune_windows(X, stats, M, order, self.window, s0, kw.get("use_rank_icir", True),
                                               kw.get("icir_threshold", -np.inf), kw.get("rho", 0.7),
                                               kw.get("top_x", 5))
-            first = _metrics_frame(M[0].cpu().numpy(), names)
-            cols = list(first.index)
-            pos = [names.index(c) for c in cols]
-            sel = pd.DataFrame(w.cpu().numpy()[:, pos], index=pd.Index(proc_dates), columns=cols)
+            with phase("D2H"):
+                m0, wh = M[0].cpu().numpy(), w.cpu().numpy()
+            with phase("dense->pandas"):
+                first = _metrics_frame(m0, names)
+                cols = list(first.index)
+                pos = [names.index(c) for c in cols]
+                sel = pd.DataFrame(wh[:, pos], index=pd.Index(proc_dates), columns=cols)
         else:
             Mh = M.cpu().numpy()
             vecs = []

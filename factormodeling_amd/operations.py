@@ -18,6 +18,7 @@ import torch
 
 from . import engine
 from .panel import device, panel_index
+from .profiling import phase
 
 __all__ = [
     "ts_sum", "ts_mean", "ts_std", "ts_zscore", "ts_rank", "ts_diff", "ts_delay", "ts_decay", "ts_backfill",
@@ -44,9 +45,13 @@ def _panel_apply(obj, fn, name=None, keep_name=True):
     """Densify ``obj`` onto the device, run ``fn(X, present)`` and gather back."""
     P = panel_index(obj.index)
     dev = device()
-    X = P.to_device(_matrix(obj), dev)
+    with phase("pandas->dense"):
+        xv = _matrix(obj)
+    X = P.to_device(xv, dev)
     Y = fn(X, P.present(dev))
-    return _wrap(obj, P.from_device(Y), name, keep_name)
+    vals = P.from_device(Y)
+    with phase("dense->pandas"):
+        return _wrap(obj, vals, name, keep_name)
 
 
 def _ew(obj, op, a=0.0, b=0.0):

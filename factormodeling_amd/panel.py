@@ -16,6 +16,8 @@ import numpy as np
 import pandas as pd
 import torch
 
+from .profiling import phase
+
 F64 = torch.float64
 
 
@@ -103,10 +105,16 @@ class PanelIndex:
         return self._present_dev[key]
 
     def to_device(self, values, device) -> torch.Tensor:
-        return torch.as_tensor(self.to_dense(values), device=device).contiguous()
+        with phase("pandas->dense"):
+            d = self.to_dense(values)
+        with phase("H2D"):
+            return torch.as_tensor(d, device=device).contiguous()
 
     def from_device(self, Y: torch.Tensor) -> np.ndarray:
-        return self.gather(Y.detach().cpu().numpy())
+        with phase("D2H"):
+            h = Y.detach().cpu().numpy()
+        with phase("dense->pandas"):
+            return self.gather(h)
 
 
 _CACHE: list = []
@@ -117,7 +125,8 @@ def panel_index(index: pd.MultiIndex) -> PanelIndex:
     for idx, p in _CACHE:
         if idx is index:
             return p
-    p = PanelIndex(index)
+    with phase("pandas->dense"):
+        p = PanelIndex(index)
     _CACHE.append((index, p))
     del _CACHE[:-8]
     return p

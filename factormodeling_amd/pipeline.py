@@ -178,10 +178,14 @@ def shard_bounds(D, world, rank, align=1):
     """Owned dates [d_lo, d_hi) of ``rank``: the ceil(D / align) blocks of ``align`` dates
     (the wide Gram's absolute date blocks, E.GRAM_DATE_BLOCK: every block then lies on one
     rank, so its exact partial is the same at any GPU count) split as evenly as whole blocks
-    allow -- rank r owns blocks [r nb / world, (r + 1) nb / world) -- so no rank is left
-    without dates while there are at least ``world`` blocks."""
+    allow -- every rank owns nb // world blocks and the first nb % world ranks one more -- so
+    no rank is left without dates while there are at least ``world`` blocks, and
+    the larger shares go to the lower ranks, the ones that send a halo (D = 121
+    over 2 ranks with a 61-date halo gives rank 0 the 61 dates it must send)."""
     nb = (D + align - 1) // align
-    b0, b1 = rank * nb // world, (rank + 1) * nb // world
+    q, rem = divmod(nb, world)
+    b0 = rank * q + min(rank, rem)
+    b1 = b0 + q + (1 if rank < rem else 0)
     return min(D, b0 * align), min(D, b1 * align)
 
 

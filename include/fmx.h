@@ -98,6 +98,9 @@ typedef int32_t fmx_status;
 /* ---- library ------------------------------------------------------------------ */
 const char* fmx_last_error(void);
 int32_t fmx_abi_version(void);
+/* "product", or "diagnostic: ..." for a development build whose kernels carry wrong-result
+ * timing arms (-DFMX_DIAG); the Python loader refuses the latter unless FMX_ALLOW_DIAG=1. */
+const char* fmx_build_variant(void);
 /* Writes "gfx950 ... CUs ... HBM bytes" of the current device into buf. */
 fmx_status fmx_device_info(char* buf, int64_t buflen);
 

@@ -92,3 +92,11 @@ def test_pairwise_schedule_matches_numpy(n):
     for scale in (1.0, 1e8, 1e-8):
         a = rng.standard_normal(n) * scale
         assert _run_schedule(blob, a) == a.sum() or (n == 0)
+
+
+def test_shipped_library_is_the_product_build():
+    """a library whose kernels carry diagnostic (wrong-result) timing arms names
+    itself through fmx_build_variant(); the shipped libfmx.so must be the product build."""
+    from factormodeling_amd import _lib
+    lib = _lib.load()
+    assert lib.fmx_build_variant().decode() == "product"

@@ -97,6 +97,55 @@ def _prune_order(summ):
     return np.argsort(-np.nan_to_num(summ[0, :, 3], nan=-np.inf), kind="stable")
 
 
+def _oracle_full_sample(P, R, L, fs):
+    """Full-sample lag-L metrics of factors ``fs`` by the oracle alone:
+    oracle.metrics.daily_stats of every target date t in [L, D) on the host pool, the n >= 3
+    rows summarized (factor_selector.py:26-73) -> [len(fs)][7]."""
+    import oracle.metrics as OM
+    import oracle_pool
+    D = R.shape[0]
+    out = np.empty((len(fs), 7))
+    for c0 in range(0, len(fs), 50):                            # 50 factors (10 GB at C2) at a time
+        sub = list(fs[c0:c0 + 50])
+        Xs = P[sub, :D - L].cpu().numpy()                       # exposures of target dates L..D-1
+        od = oracle_pool.daily_many(Xs, R[L:])
+        del Xs
+        for k in range(len(sub)):
+            ok = od[k, :, 0] >= 3
+            out[c0 + k] = OM.summarize(od[k, ok, 1], od[k, ok, 2], od[k, ok, 3])
+    return out
+
+
+def _check_summ(summ, vals, fs, what):
+    """The step's full-sample metrics of factors fs vs the oracle's (<= 1e-9)."""
+    got = summ[0][fs][:, [0, 1, 2, 3, 4, 6]]
+    assert_close(got.ravel(), vals[:, [0, 1, 2, 3, 4, 6]].ravel(), rtol=1e-9, atol=1e-12,
+                 what=f"{what} full-sample metrics")
+
+
+def _plain_corr(X, chunk=126):
+    """C of every factor pair in plain fp64 on the device (oracle/gram.py's spec: per-date
+    z-scores with ddof 0, NaN / sigma 0 -> invalid, C = sum ZZ' / sum MM'), summed over date
+    chunks -- independent of the exact-limb Gram it checks."""
+    import torch
+    F, D, A = X.shape
+    G = torch.zeros((F, F), dtype=torch.float64, device=X.device)
+    N = torch.zeros_like(G)
+    for d0 in range(0, D, chunk):
+        x = X[:, d0:d0 + chunk]
+        m = ~torch.isnan(x)
+        n = m.sum(2, keepdim=True)
+        mu = torch.where(m, x, 0.0).sum(2, keepdim=True) / n
+        sd = torch.sqrt(torch.where(m, (x - mu) ** 2, 0.0).sum(2, keepdim=True) / n)
+        ok = m & (sd > 0)
+        z = torch.where(ok, (x - mu) / sd, 0.0).reshape(F, -1)
+        mf = ok.to(torch.float64).reshape(F, -1)
+        G += z @ z.T
+        N += mf @ mf.T
+        del x, m, z, mf, ok
+    return torch.where(N > 0, G / N, torch.zeros_like(G)).cpu().numpy()
+
+
 @pytest.mark.timeout(900)
 def test_c2_full_step_sampled_vs_oracle(dev):
     import torch
@@ -170,7 +219,17 @@ def test_c2_full_step_sampled_vs_oracle(dev):
         assert n > 0
         np.testing.assert_allclose(C[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
         assert C[a, b] == C[b, a]
-    assert kept == _greedy(C, _prune_order(col["summ"].cpu().numpy()), cfg.prune_rho, cfg.top_x)
+    summ = col["summ"].cpu().numpy()
+    assert kept == _greedy(C, _prune_order(summ), cfg.prune_rho, cfg.top_x)
+    # the pruning order pinned to the oracle alone -- every factor's
+    # full-sample lag-1 metrics recomputed from the raw panel (all 2519 target dates), the
+    # order they give equal to the step's, and the kept set walked over the oracle's order
+    L0 = cfg.ic_lags[0]
+    vals = _oracle_full_sample(sp.X, R, L0, list(range(F)))
+    _check_summ(summ, vals, list(range(F)), "C2")
+    oorder = OM.nargsort_desc(vals[:, 3])
+    assert np.array_equal(oorder, _prune_order(summ)), "C2 pruning order vs the oracle"
+    assert kept == _greedy(C, oorder, cfg.prune_rho, cfg.top_x)
     del sp, col, w
 
 
@@ -197,7 +256,20 @@ def test_c4_full_wide_gram(dev):
     for a, b in pairs:
         g, n = _zgram(sp.X[a], sp.X[b])
         np.testing.assert_allclose(Cn[a, b], g / n, rtol=1e-10, atol=1e-12, err_msg=f"C[{a},{b}]")
-    assert kept == _greedy(Cn, _prune_order(col["summ"].cpu().numpy()), cfg.prune_rho, None)
+    summ = col["summ"].cpu().numpy()
+    dorder = _prune_order(summ)
+    assert kept == _greedy(Cn, dorder, cfg.prune_rho, None)
+    # the first 32 factors of the pruning order and 32 others, their
+    # full-sample metrics by the oracle alone; their relative order under the oracle's values
+    # equals the step's order restricted to them
+    others = rng.choice(dorder[32:], 32, replace=False)
+    fs = [int(f) for f in dorder[:32]] + [int(f) for f in others]
+    vals = _oracle_full_sample(sp.X, sp.R.cpu().numpy(), cfg.ic_lags[0], fs)
+    _check_summ(summ, vals, fs, "C4")
+    sub = np.asarray(fs)[OM.nargsort_desc(vals[:, 3])]
+    pos = np.empty(F, dtype=np.int64)
+    pos[dorder] = np.arange(F)
+    assert np.array_equal(sub, np.asarray(fs)[np.argsort(pos[fs], kind="stable")]), "C4 order vs the oracle"
     # the daily IC the pruning order comes from, on sampled (factor, date) pairs across the
     # whole panel (rows past 4.19M of a 1-D grid of 1024-thread rows once went unwritten)
     daily = col["daily"]
@@ -210,6 +282,57 @@ def test_c4_full_wide_gram(dev):
         assert got[0] == n, (f, t)
         assert_close(got[1:], np.array([ic, ric, beta]), rtol=1e-9, atol=1e-12, what=f"C4 IC f{f} t{t}")
     del sp, col, C, daily
+
+
+@pytest.mark.timeout(900)
+def test_c2_correlated_zoo_prune_vs_oracle(dev):
+    """a full-size C2 panel whose factors are correlated (each a random
+    mix of 6 common factors plus noise, the SURVEY 8(d) NaN mask kept), pruned over the whole
+    ordered zoo so that the walk rejects factors.  The kept set must equal the greedy walk of
+    a plain fp64 C over the ORACLE's order (full-sample lag-1 rank_IC_IR of every factor from
+    oracle.metrics.daily_stats); no walk decision may sit within 1e-9 of rho."""
+    import dataclasses
+    import torch
+    import oracle.metrics as OM
+    from factormodeling_amd import pipeline as PL
+    D, A, F = 2520, 5000, 200
+    cfg = dataclasses.replace(PL.workload_config("c2"), prune_top_x=None)
+    sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=3, halo=cfg.halo)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    K = 6
+    mix = torch.randn((F, K), generator=g, dtype=torch.float64, device=dev)
+    for d0 in range(0, D, 252):                                # in place, 252 dates at a time
+        base = torch.randn((K, min(252, D - d0), A), generator=g, dtype=torch.float64, device=dev)
+        noise = torch.randn((F, base.shape[1], A), generator=g, dtype=torch.float64, device=dev)
+        z = torch.einsum("fk,kda->fda", mix, base) + 0.6 * noise
+        x = sp.X[:, d0:d0 + base.shape[1]]
+        x.copy_(torch.where(torch.isnan(x), x, z))
+        del base, noise, z
+    col = {"_factors": [0]}
+    _, kept = PL.run_step(sp, cfg, collect=col)
+    torch.cuda.synchronize()
+    summ = col["summ"].cpu().numpy()
+    Cdev = col["C"].cpu().numpy()
+    del col
+    import factormodeling_amd.engine as E
+    E._WORK.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+    Cp = _plain_corr(sp.X)
+    np.testing.assert_allclose(Cdev, Cp, rtol=1e-10, atol=1e-12)
+    vals = _oracle_full_sample(sp.X, sp.R.cpu().numpy(), cfg.ic_lags[0], list(range(F)))
+    _check_summ(summ, vals, list(range(F)), "C2 zoo")
+    oorder = OM.nargsort_desc(vals[:, 3])
+    assert np.array_equal(oorder, _prune_order(summ)), "C2 zoo pruning order vs the oracle"
+    walk = _greedy(Cp, oorder, cfg.prune_rho, None)
+    assert kept == walk
+    assert 0 < len(walk) < F // 2, f"the zoo should be pruned hard ({len(walk)} kept)"
+    for i, f in enumerate(oorder):                             # decisions clear of rho
+        prior = [k for k in walk if list(oorder).index(k) < i]
+        if prior:
+            assert abs(np.max(np.abs(Cp[f, prior])) - cfg.prune_rho) > 1e-9, f
+    del sp
 
 
 @pytest.mark.timeout(900)

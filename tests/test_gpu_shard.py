@@ -239,3 +239,43 @@ def test_c5_sharded_step_selection_matches_one_shard(dev, world):
         np.testing.assert_allclose(feat, col1["feature"][:, lo:hi], rtol=1e-12, atol=1e-14, equal_nan=True)
         np.testing.assert_allclose(daily, col1["daily"], rtol=1e-12, atol=1e-14, equal_nan=True)
         assert np.array_equal(w, w1), lo
+
+
+_BR_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from factormodeling_amd import pipeline as PL
+from factormodeling_amd.comm import run_local_shards
+dev = torch.device("cuda", 0)
+D, A, F = 120, 700, 6
+cfg = PL.StepConfig(sel_window=40)
+sp = PL.ShardedPanel(D, A, F, 0, 1, dev, seed=5, halo=cfg.halo)
+col1 = {}
+w1, kept1 = PL.run_step(sp, cfg, collect=col1)
+torch.cuda.synchronize()
+def shard(rank, comm):
+    s = PL.ShardedPanel(D, A, F, device=dev, seed=5, halo=cfg.halo, comm=comm)
+    col = {}
+    w, kept = PL.run_step(s, cfg, collect=col)
+    torch.cuda.current_stream().synchronize()
+    return w.cpu().numpy(), kept, col["daily"].cpu().numpy()
+for w, kept, daily in run_local_shards(2, shard):
+    assert np.array_equal(w, w1.cpu().numpy()) and kept == kept1
+    assert np.array_equal(daily, col1["daily"].cpu().numpy(), equal_nan=True)
+print("OK")
+"""
+
+
+@pytest.mark.timeout(300)
+def test_sharded_step_under_br_rank_impl(dev):
+    """with the splitter-bucket rank kernels (FMX_RANK_IMPL=br, read once per
+    process: a child process) the fused date-range entry falls back to the two-pass form
+    factor by factor instead of raising; the 2-shard step equals the 1-shard step."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMX_RANK_IMPL="br")
+    r = subprocess.run([sys.executable, "-c", _BR_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

@@ -132,6 +132,13 @@ def test_shard_bounds_cover_dates():
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
         assert all(hi > lo for lo, hi in spans) and all(lo % B == 0 for lo, _ in spans)
         PL.check_sharding(D, world, 1, B)
+    # the larger shares go to the lower (halo-sending) ranks -- D = 121 over 2
+    # ranks with a 61-date halo: rank 0 owns the 61 dates it sends
+    assert PL.shard_bounds(121, 2, 0) == (0, 61) and PL.shard_bounds(121, 2, 1) == (61, 121)
+    PL.check_sharding(121, 2, 61)
+    for D, world in ((121, 2), (2520, 7), (203, 8), (33, 3)):
+        n = [hi - lo for lo, hi in (PL.shard_bounds(D, world, r) for r in range(world))]
+        assert n == sorted(n, reverse=True) and max(n) - min(n) <= 1, (D, world, n)
 
 
 def test_rank_owning_fewer_dates_than_halo_is_rejected():
