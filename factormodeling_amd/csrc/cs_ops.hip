@@ -935,8 +935,12 @@ extern "C" fmx_status fmx_cs_rank_winsor(const double* X, double* Yrank, double*
   if (F == 0 || D == 0 || A == 0) return FMX_OK;
   fmx_status e = br_cs_rank_winsor(X, Yrank, Ywinsor, F, D, A, ld, qlo, qhi, present, rank2, as_stream(stream));
   if (e != FMX_ERR_UNSUPPORTED) return e;
-  if (rank2) { set_error("rank2 needs the fused rank kernel (A <= 16384)"); return FMX_ERR_UNSUPPORTED; }
-  // rows the fused kernel does not take: the two single-op passes
+  // rows the fused kernel does not take (FMX_RANK_IMPL=br, or its LDS does not fit): the
+  // doubled ranks from the ranks-only pass, then the two single-op passes
+  if (rank2) {
+    if (A > 16384) { set_error("rank2 needs the fused rank kernel (A <= 16384)"); return FMX_ERR_UNSUPPORTED; }
+    if ((e = br_cs_rank2(X, rank2, F, D, A, ld, 0, D, as_stream(stream)))) return e;
+  }
   if ((e = fmx_cs_rank(X, Yrank, F, D, A, ld, FMX_RANK_AVERAGE, present, stream))) return e;
   return cs_quantile(0, X, Ywinsor, F, D, A, ld, qlo, qhi, present, stream);
 }

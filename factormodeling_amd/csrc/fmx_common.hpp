@@ -86,6 +86,27 @@ __device__ __forceinline__ double mdiv(double x, double n, double r) {
   return __builtin_fma(rem, r, q0);
 }
 
+// RN(x / b) for a GENERAL divisor b from r = RN(1 / b) (Markstein's theorem: r within 1/2 ulp
+// of 1/b and q0 = RN(x r) within 1 ulp of x / b make rem = x - q0 b exact under an fma and
+// RN(q0 + rem r) the correctly rounded quotient) -- for a row-uniform divisor such as a
+// cross-sectional standard deviation, 3 fp64 ops per element in place of the IEEE divide
+// sequence.  Range guards (integer tests of exponent fields): b_ok = rdiv_ok(b) keeps b in
+// [2^-800, 2^800] (computed once per row); x below 2^-895 (zero included) and q0 outside
+// [2^-959, 2^936] or non-finite take the IEEE divide -- no intermediate under/overflow.
+// tests/native/rdiv_check.c: 1e8 host cases bit-identical to x / b.
+__device__ __forceinline__ bool rdiv_ok(double b) {
+  const uint32_t e = ((uint32_t)__double2hiint(b) >> 20) & 0x7ffu;
+  return e - (1023u - 800u) <= 1600u;
+}
+__device__ __forceinline__ double rdiv(double x, double b, double r, bool b_ok) {
+  const double q0 = x * r;
+  const uint32_t eq = ((uint32_t)__double2hiint(q0) >> 20) & 0x7ffu;
+  const uint32_t ex = ((uint32_t)__double2hiint(x) >> 20) & 0x7ffu;
+  if (!b_ok || eq - 64u > 1958u - 64u || ex < 128u) return x / b;
+  const double rem = __builtin_fma(-q0, b, x);
+  return __builtin_fma(rem, r, q0);
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Row kernels launch their F * D (or D * F) rows as a 2-D grid dim3(inner, outer) and read

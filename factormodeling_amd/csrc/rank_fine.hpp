@@ -490,13 +490,15 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     BR_PH();
     const double sd = sqrt(var);
     const bool g2 = sd == 0.0 || sd != sd;     // neutralize: sigma in {0, NaN} -> 0
+    const double rsd = 1.0 / sd;               // (x - mean) / sd by rdiv: bit-identical
+    const bool sd_ok = rdiv_ok(sd);
     double* yz = zn.Yz + row * ld;
     double* yn = zn.Yn + row * ld;
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) {
       if (!fr_in<NT>(t, k, (int)A)) continue;
       const int ia = fr_opaque(t) + k * NT;
-      const double o = (vrow[ia] - mean) / sd;
+      const double o = rdiv(vrow[ia] - mean, sd, rsd, sd_ok);
       __builtin_nontemporal_store(o, yz + ia);
       __builtin_nontemporal_store(g2 ? 0.0 : o, yn + ia);
     }
@@ -685,13 +687,21 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     const int lt = le[k] & 0xffff, eq = le[k] >> 16;
     const int less = (sl[k] & 0xffff) + lt;
     if constexpr (IC) r2[k / 2] |= (key[k] != KEY_SENTINEL ? (uint32_t)(2 * less + eq + 1) : 0u) << (16 * (k % 2));
-    double r;
-    if (method == FMX_RANK_MIN) r = (double)(less + 1);
-    else if (method == FMX_RANK_MAX) r = (double)(less + eq);
-    else r = (double)less + (double)(eq + 1) / 2.0;
     // write-once outputs: nontemporal stores
     const int ia = fr_opaque(t) + k * NT;       // recomputed here, not kept from the loads
-    if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : mdiv(r - 1.0, den, rden), y + ia);
+    if constexpr (ZN) {
+      // method average: (r - 1) / den with r = r2 / 2, r2 = 2 less + eq + 1 the doubled rank;
+      // (r2 - 2) / (2 den) is the same real number (r - 1 = (r2 - 2) / 2 exactly), so
+      // mdiv(r2 - 2, 2 den, RN(1 / den) / 2) gives the same bits from one conversion
+      const double q = mdiv((double)(2 * less + eq - 1), 2.0 * den, 0.5 * rden);
+      __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : q, y + ia);
+    } else {
+      double r;
+      if (method == FMX_RANK_MIN) r = (double)(less + 1);
+      else if (method == FMX_RANK_MAX) r = (double)(less + eq);
+      else r = (double)less + (double)(eq + 1) / 2.0;
+      if (Y) __builtin_nontemporal_store(key[k] == KEY_SENTINEL ? qnan() : mdiv(r - 1.0, den, rden), y + ia);
+    }
     if (RK) __builtin_nontemporal_store((fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1)),
                                         RK + row * ld + ia);
     if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {

@@ -102,9 +102,11 @@ __global__ void __launch_bounds__(64 * ICW_WAVES, ICW_MINW)
 k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, const double* __restrict__ Rt, int64_t F,
           int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
           const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
-  // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64);
-  // T[b] = start | end << 16 of its E entries in eb) and the entries eb[ICW_EC] grouped by
-  // block.  Dynamic LDS: ICW_WAVES * 2 * (nbp + ICW_EC) + 2 words.
+  // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64))
+  // and the entries eb[ICW_EC] grouped by block.  T[b] is 64-bit: start | count << 16 of
+  // its E entries in eb, and the block's first two entries (<< 32, << 48; entries are
+  // doubled ranks in [2, 2A], 16 bits): one ds_read_b64 per lag and element instead of the
+  // table word plus two entry reads.  Dynamic LDS: ICW_WAVES * 2 * (2 nbp + ICW_EC) + 2 words.
   extern __shared__ uint32_t icw_lds[];
   __shared__ double scr[ICW_WAVES * 32];
   // the wave index as a scalar: the row, its pointers and lags live in SGPRs (saddr loads)
@@ -125,12 +127,14 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   const fmx_rank2_t* rkf = RK + (f * D + s) * ld;
   const int nb = (int)((2 * A) >> 6) + 1;     // doubled ranks are <= 2A
   const int nbp = (nb + 1) & ~1;
-  uint32_t* T[2];
+  uint32_t* T[2];                             // counts during the build (u32 view of T64)
+  uint64_t* T64[2];
   uint32_t* eb[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    T[m] = icw_lds + (wid * 2 + m) * (nbp + ICW_EC);
-    eb[m] = T[m] + nbp;
+    T[m] = icw_lds + (wid * 2 + m) * (2 * nbp + ICW_EC);
+    T64[m] = reinterpret_cast<uint64_t*>(T[m]);
+    eb[m] = T[m] + 2 * nbp;
   }
   // 1. E lists: the doubled ranks of the valid exposures at the target date's NaN-return
   // positions (key(e) < key(x) <=> RK(e) < RK(x), ties alike, so the corrections can be
@@ -165,7 +169,7 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   for (int s = 0; s < ICW_PF; ++s) load(64 * s, s);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    for (int b = lane; b < nbp; b += 64) T[m][b] = 0u;
+    for (int b = lane; b < nbp; b += 64) T64[m][b] = 0ull;
 #pragma unroll
     for (int q = 0; q < ICW_EC / 64; ++q) { er[m][q] = 0u; es[m][q] = 0; }
   }
@@ -210,12 +214,16 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     if (ne[m] == 0) continue;                 // wave-uniform
-    // exclusive scan of the block counts: lane l owns blocks [l R, l R + R)
+    // exclusive scan of the block counts: lane l owns blocks [l R, l R + R) (R <= 9: A <= 16384)
+    constexpr int RMAX = 9;
     const int R = (nbp + 63) >> 6;
+    int cn[RMAX];
     int loc = 0;
-    for (int q = 0; q < R; ++q) {
+#pragma unroll
+    for (int q = 0; q < RMAX; ++q) {
       const int b = lane * R + q;
-      loc += b < nbp ? (int)T[m][b] : 0;
+      cn[q] = (q < R && b < nbp) ? (int)T[m][b] : 0;   // the u32 counts, read before T64 is written
+      loc += cn[q];
     }
     int incl = loc;
 #pragma unroll
@@ -224,18 +232,32 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
       if (lane >= o) incl += u;
     }
     int run = incl - loc;
-    for (int q = 0; q < R; ++q) {
+    int st[RMAX];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < RMAX; ++q) {
       const int b = lane * R + q;
-      if (b < nbp) {
-        const int n = (int)T[m][b];
-        T[m][b] = (uint32_t)run | ((uint32_t)(run + n) << 16);
-        run += n;
-      }
+      st[q] = run;
+      if (q < R && b < nbp) T64[m][b] = (uint64_t)((uint32_t)run | ((uint32_t)cn[q] << 16));
+      run += cn[q];
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int q = 0; q < ICW_EC / 64; ++q)
-      if (er[m][q]) eb[m][(T[m][er[m][q] >> 6] & 0xffffu) + es[m][q]] = er[m][q];
+      if (er[m][q]) eb[m][((uint32_t)T64[m][er[m][q] >> 6] & 0xffffu) + es[m][q]] = er[m][q];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // the first two entries of each block into its table word
+#pragma unroll
+    for (int q = 0; q < RMAX; ++q) {
+      const int b = lane * R + q;
+      if (q < R && b < nbp && cn[q] > 0) {
+        const uint64_t e0 = eb[m][st[q]], e1 = cn[q] > 1 ? eb[m][st[q] + 1] : 0u;
+        T64[m][b] = (uint64_t)((uint32_t)st[q] | ((uint32_t)cn[q] << 16)) | (e0 << 32) | (e1 << 48);
+      }
+    }
   }
   __builtin_amdgcn_wave_barrier();
   // 2. one pass.  Per lag: pair count (ballots); the first pair's (x, r) is the lag's
@@ -279,10 +301,11 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   // one, and a loop there made the whole wave run it (7.75 -> 7.30 ms at C2; a read past the
   // list end is masked, and the LDS region is padded by 2)
   auto pair_rank = [&](int m, uint32_t rk) {
-    const uint32_t tb = T[m][rk >> 6];
-    const uint32_t j0 = tb & 0xffffu, j1 = tb >> 16, nj = j1 - j0;
+    const uint64_t tb = T64[m][rk >> 6];
+    const uint32_t lo = (uint32_t)tb, hi = (uint32_t)(tb >> 32);
+    const uint32_t j0 = lo & 0xffffu, nj = lo >> 16, j1 = j0 + nj;
+    const uint32_t e0 = hi & 0xffffu, e1 = hi >> 16;
     int corr = 2 * (int)j0;
-    const uint32_t e0 = eb[m][j0], e1 = eb[m][j0 + 1];
     corr += nj > 0 ? (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) : 0;
     corr += nj > 1 ? (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0) : 0;
     for (uint32_t j = j0 + 2; j < j1; ++j) {   // a third entry or more (rare)
@@ -432,7 +455,7 @@ fmx_status br_ic_ranked(const double* X, const fmx_rank2_t* RK, const double* R,
     FMX_LAUNCH_CHECK("k_ic_empty");
     FMX_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
     const int nbp = ((int)((2 * A) >> 6) + 2) & ~1;
-    const size_t lds = sizeof(uint32_t) * (ICW_WAVES * 2 * (size_t)(nbp + ICW_EC) + 2);   // + 2: k_ic_wave's e1 read
+    const size_t lds = sizeof(uint32_t) * (ICW_WAVES * 2 * (size_t)(2 * nbp + ICW_EC) + 2);
     k_ic_wave<<<wave_grid, 64 * ICW_WAVES, lds, st>>>(X, RK, R, F, D, A, ld, L0, L1, NL, o, pos, npos, ovf);
     FMX_LAUNCH_CHECK("k_ic_wave");
     void* args[] = {(void*)&X, (void*)&RK, (void*)&R, (void*)&F, (void*)&D, (void*)&A, (void*)&ld, (void*)&L0,

@@ -106,8 +106,12 @@ class FactorSelector:
         self.method = method
         self.method_kwargs = method_kwargs or {}
         self.factor_selection = None
-        self.dates = sorted(list(set(factors_df.index.get_level_values("date")).intersection(
-            set(self.factor_ret_df.index))))
+        # the reference's sorted(set(dates) & set(factor_ret_df.index)) (factor_selector.py:91)
+        # on the distinct dates only: a Python set of every (date, symbol) row's Timestamp took
+        # 14 s of the 2520 x 5000 drop-in call (profiles/r06/dropin_c2s_*.json)
+        fd = pd.Index(factors_df.index.get_level_values("date").unique())
+        common = fd.intersection(pd.Index(self.factor_ret_df.index).unique())
+        self.dates = sorted(common.tolist())
         logger.info("FactorSelector initialized.")
 
     @property

@@ -21,3 +21,18 @@ def test_mdiv_matches_ieee_division(tmp_path):
     p = subprocess.run([str(exe), "4096", "20000"], capture_output=True, text=True)
     assert p.returncode == 0, p.stderr + p.stdout
     assert "0 mismatches" in p.stdout
+
+
+def test_rdiv_matches_ieee_division(tmp_path):
+    """fmx_common.hpp rdiv (the cross-sectional z-scores' (x - mean) / sd from RN(1 / sd):
+    Markstein's correction for a general divisor, with its range guards) == the IEEE
+    quotient on 1e8 host cases (tests/native/rdiv_check.c)."""
+    exe = tmp_path / "rdiv_check"
+    try:
+        subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), os.path.join(HERE, "native", "rdiv_check.c"),
+                        "-lm"], check=True, capture_output=True)
+    except (OSError, subprocess.CalledProcessError) as e:
+        pytest.skip(f"no host C compiler: {e}")
+    p = subprocess.run([str(exe), "25000", "4000"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr + p.stdout
+    assert "0 mismatches" in p.stdout
