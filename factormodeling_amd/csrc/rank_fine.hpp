@@ -473,17 +473,19 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     int cnt = An; (void)sch; table();
     const double s1 = vrow[t], mean = s1, s2 = vrow[t + 1], var = s2;
 #else
-    int cnt, c2;
+    // the non-NaN count is the rank phase's #valid keys (its ballots, in wred since the
+    // barrier above): no per-element count in the moment leaves
+    int c1, c2, cnt = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cnt += (int)wred[w].y;
     const double s1 = block_pw_sum_w0<NT>([&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; },
-                                          [&](int i) { return (int)(vrow[i] == vrow[i]); }, sch, zn_nodes,
-                                          zn_iscr, &cnt, table);
+                                          [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c1, table);
     const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
     BR_PH();
+    // (mean - u)^2 for a valid u, 0 for NaN: numpy's (mean - where(nan, 0, u))^2 masked to 0
     const double s2 = block_pw_sum_w0<NT>([&](int i) {
       const double u = vrow[i];
-      const double z = u == u ? u : 0.0;
-      const double q = (mean - z) * (mean - z);
-      return u == u ? q : 0.0;
+      return u == u ? (mean - u) * (mean - u) : 0.0;
     }, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
     const double var = cnt > 0 ? s2 / (double)cnt : qnan();
 #endif

@@ -512,15 +512,17 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
   __builtin_amdgcn_sched_barrier(0);   // keep the unrolled steps' live ranges apart
 }
 
-template <int W, int WR, int PF>
-__global__ void __launch_bounds__(256, TS_SET_WAVES)
+// NT: columns (lanes) per workgroup -- adjacent assets, so one date row of a workgroup is
+// NT * 8 contiguous bytes per stream (FMX_TS_SET_NT=512|1024 for A/B; 256 by default)
+template <int W, int WR, int PF, int NT = 256>
+__global__ void __launch_bounds__(NT, TS_SET_WAVES)
 k_ts_set(const double* __restrict__ X, double* __restrict__ Ym, double* __restrict__ Ys, double* __restrict__ Yz,
          double* __restrict__ Yr, double* __restrict__ Yd, int64_t F, int64_t D, int64_t A, int64_t ld) {
   static_assert(W % PF == 0 && WR >= 1 && WR <= W, "windows");
   __shared__ double rt[W + 1];                // RN(1 / k), k <= W (mdiv)
-  for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+  for (int k = threadIdx.x; k <= W; k += NT) rt[k] = 1.0 / (double)k;
   __syncthreads();
-  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t col = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (col >= F * A) return;
   const int64_t f = col / A, a = col - f * A;
   const int64_t off0 = f * D * ld + a;
@@ -1050,8 +1052,9 @@ k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, do
 // (k_ts_cvf_rl's VarSt, same order), so the feature
 //     sign(corr) * (x / ts_std(x, W))      (ts_std 0 -> NaN; np.sign of a NaN corr is NaN)
 // is written while the corr is in registers: the corr panel is not written and read back,
-// and x / x[d - W] are read once for both.  C (optional) also receives the corr.
-template <int PF>
+// and x / x[d - W] are read once for both.  C (optional, WC) also receives the corr.
+//
+template <int PF, bool WC>
 __global__ void __launch_bounds__(256)
 k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ C,
                double* __restrict__ Out, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W,
@@ -1065,27 +1068,33 @@ k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, do
   const double* x = X + f * D * ld + a;
   const double* yc = Ycol + f * y_fstride + a;
   double* o = Out + f * D * ld + a;
-  double* cp = C ? C + f * D * ld + a : nullptr;
+  double* cp = WC ? C + f * D * ld + a : nullptr;
   MeanSt mxy;
   MVSt sx, sy;
   VarSt vs;                                       // ts_std(x, W) of the raw x (the feature's)
   int64_t i = 0, cnt = 0;
   bool first = true;
+  // software pipeline: the four loads of date d + PF are issued before date d is computed
+  // (a ring of PF dates in registers), so each wave keeps a date's HBM / MALL latency in
+  // flight across its own arithmetic instead of waiting at the top of every step
+  double nx[PF], ny[PF], nxo[PF], nyo[PF];
+  auto fetch = [&](int64_t d, int s) {
+    const bool in = d < D, old = in && d >= W;
+    nx[s] = in ? x[d * ld] : 0.0;
+    ny[s] = in ? yc[d * ld] : 0.0;
+    nxo[s] = old ? x[(d - W) * ld] : 0.0;
+    nyo[s] = old ? yc[(d - W) * ld] : 0.0;
+  };
+#pragma unroll
+  for (int q = 0; q < PF; ++q) fetch(q, q);
   for (int64_t d0 = 0; d0 < D; d0 += PF) {
     double xr[PF], yr[PF], xo[PF], yo[PF];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int64_t d = d0 + q;
-      xr[q] = d < D ? x[d * ld] : 0.0;
-      yr[q] = d < D ? yc[d * ld] : 0.0;
-      const bool old = d < D && d >= W;
-      xo[q] = old ? x[(d - W) * ld] : 0.0;
-      yo[q] = old ? yc[(d - W) * ld] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t d = d0 + q;
       if (d >= D) break;
+      xr[q] = nx[q]; yr[q] = ny[q]; xo[q] = nxo[q]; yo[q] = nyo[q];
+      fetch(d + PF, q);
       const double xv = xr[q] + 0.0 * yr[q];
       const double yv = yr[q] + 0.0 * xr[q];
       const double pv = xv * yv;
@@ -1102,12 +1111,20 @@ k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, do
       const double cc = (double)cnt;
       const double ratio = cnt >= 2 ? mdiv(cc, cc - 1.0, rt[cnt - 1]) : cc / (cc - 1.0);
       const double num = (mxy.result_r(W, rt) - sx.mean_r(W, rt) * sy.mean_r(W, rt)) * ratio;
-      const double den = sqrt(sx.var_r(W, 1, rt) * sy.var_r(W, 1, rt));
-      const double cq = num / den;
-      if (cp) __builtin_nontemporal_store(cq, cp + d * ld);
+      const double pv2 = sx.var_r(W, 1, rt) * sy.var_r(W, 1, rt);
+      double sg;
+      if constexpr (WC) {
+        const double cq = num / sqrt(pv2);
+        __builtin_nontemporal_store(cq, cp + d * ld);
+        sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
+      } else {
+        // (a sign-only shortcut that skips the sqrt and divide for ordinary num / p measured
+        // neutral, 3.35 vs 3.33 ms per 252 dates: this pass is not bound by those VALU ops)
+        const double cq = num / sqrt(pv2);
+        sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
+      }
       double sd = zsqrt(vs.var_r(W, 1, rt));
       if (sd == 0.0) sd = qnan();
-      const double sg = cq > 0.0 ? 1.0 : (cq < 0.0 ? -1.0 : (cq == 0.0 ? 0.0 : cq));
       __builtin_nontemporal_store(sg * (xr[q] / sd), o + d * ld);
       i += 1;
     }
@@ -1349,8 +1366,14 @@ extern "C" fmx_status fmx_ts_set(const double* X, double* Ymean, double* Ystd, d
   if (!present && window == 20 && rank_window == 10 && getenv("FMX_TS_SET_SPLIT") == nullptr) {
     void* args[] = {(void*)&X, (void*)&Ymean, (void*)&Ystd, (void*)&Yzscore, (void*)&Yrank, (void*)&Ydecay,
                     (void*)&F, (void*)&D, (void*)&A, (void*)&ld};
-    FMX_HIP(hipLaunchKernel((const void*)k_ts_set<20, 10, 5>, dim3((unsigned)ceil_div(F * A, 256)), dim3(256), args,
-                            0, as_stream(stream)));
+    static const int nt = [] {
+      const char* e = getenv("FMX_TS_SET_NT");
+      const int v = e ? atoi(e) : 256;
+      return (v == 512 || v == 1024) ? v : 256;
+    }();
+    const void* k = nt == 1024 ? (const void*)k_ts_set<20, 10, 5, 1024>
+                    : nt == 512 ? (const void*)k_ts_set<20, 10, 5, 512> : (const void*)k_ts_set<20, 10, 5, 256>;
+    FMX_HIP(hipLaunchKernel(k, dim3((unsigned)ceil_div(F * A, nt)), dim3(nt), args, 0, as_stream(stream)));
     return FMX_OK;
   }
   // other windows / ragged panels: the three moments from one pair of machines (one pass),
@@ -1441,7 +1464,9 @@ extern "C" fmx_status fmx_ts_corr_feature(const double* X, const double* Ycol, d
     const char* e = getenv("FMX_CORR_FEAT_PF");
     return e && e[0] == '2';
   }();
-  FMX_HIP(hipLaunchKernel(pf2 ? (const void*)k_ts_corr_feat<2> : (const void*)k_ts_corr_feat<1>,
+  const void* k = C ? (pf2 ? (const void*)k_ts_corr_feat<2, true> : (const void*)k_ts_corr_feat<1, true>)
+                    : (pf2 ? (const void*)k_ts_corr_feat<2, false> : (const void*)k_ts_corr_feat<1, false>);
+  FMX_HIP(hipLaunchKernel(k,
                           dim3((unsigned)(nab * ceil_div(F, 4))), dim3(256), args, sizeof(double) * (W + 1),
                           as_stream(stream)));
   return FMX_OK;

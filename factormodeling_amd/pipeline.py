@@ -551,25 +551,33 @@ def run_ret_ops(sp, cfg, timers=None, be=ENGINE, collect=None):
     (fmx_ts_corr_feature; a backend without it: ts_corr into a chunk buffer, then
     fmx_ts_corr_vol_feature), which the rest of the step runs on."""
     F = sp.X.shape[0]
-    fc = cfg.factor_chunk or F
-    n = min(fc, F)
-    bufs = getattr(sp, "ret_bufs", None)
-    if bufs is None or bufs[0].shape[0] != n or len(bufs) != len(cfg.ret_ops):
-        bufs = [torch.empty((n,) + tuple(sp.X.shape[1:]), dtype=sp.X.dtype, device=sp.X.device)
-                for _ in cfg.ret_ops]
-        sp.ret_bufs = bufs
+    fused = lambda op, w: op == "corr_vol" and hasattr(be, "corr_feature_into") and w <= getattr(  # noqa: E731
+        be, "corr_feature_max_w", E.CORR_FEATURE_MAX_W)
+    want_corr = collect is not None and collect.get("_factors") is None
+    if all(fused(op, w) for op, w in cfg.ret_ops) and not want_corr:
+        # every op is the one-pass corr -> feature writing straight into sp.feature: no
+        # scratch, so no chunks -- one launch over all factors (five 100-factor launches
+        # each ended on a part-filled round of workgroups)
+        fc, bufs = F, [None] * len(cfg.ret_ops)
+    else:
+        fc = cfg.factor_chunk or F
+        n = min(fc, F)
+        bufs = getattr(sp, "ret_bufs", None)
+        if bufs is None or bufs[0].shape[0] != n or len(bufs) != len(cfg.ret_ops):
+            bufs = [torch.empty((n,) + tuple(sp.X.shape[1:]), dtype=sp.X.dtype, device=sp.X.device)
+                    for _ in cfg.ret_ops]
+            sp.ret_bufs = bufs
     if any(op == "corr_vol" for op, _ in cfg.ret_ops) and getattr(sp, "feature", None) is None:
         sp.feature = torch.empty_like(sp.X)
     for f0 in range(0, F, fc):
         f1 = min(F, f0 + fc)
         Xc = sp.X[f0:f1]
         for (op, w), buf in zip(cfg.ret_ops, bufs):
-            out = buf[: f1 - f0]
+            out = buf[: f1 - f0] if buf is not None else None
             t0 = _ev(timers)
-            if op == "corr_vol" and hasattr(be, "corr_feature_into") and w <= getattr(
-                    be, "corr_feature_max_w", E.CORR_FEATURE_MAX_W):
+            if fused(op, w):
                 # one pass: the corr stays in registers (written only when collected)
-                want = collect is not None and collect.get("_factors") is None
+                want = want_corr
                 be.corr_feature_into(Xc, sp.R, w, sp.feature[f0:f1], out if want else None)
                 _rec(timers, f"ret:corr_vol:{w}", t0)
                 if want:

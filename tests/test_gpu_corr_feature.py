@@ -26,6 +26,9 @@ def _panel(F, D, A, seed):
     X[0, 10:40, :5] = 1.25                        # constant windows: std 0 -> NaN feature
     X[0, :, 5] = 0.0                              # exact zeros
     X[1 % F, 50, 6:9] = np.inf
+    if F >= 5:                                    # extreme exponents: the sign-only fast path's
+        X[2] *= 1e-200                            # guards (|num| < 2^-500, vx vy > 2^501) send
+        X[3] *= 1e150                             # these to the full num / sqrt(vx vy)
     R = 0.01 * rng.standard_normal((D, A))
     R[rng.random(R.shape) < 0.05] = np.nan
     R[30:33, 10:14] = np.nan                      # return gaps inside the window
