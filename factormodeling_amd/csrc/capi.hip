@@ -185,6 +185,17 @@ int pw_len(int n) {
 }  // namespace fmx
 
 // Test hook: copy the schedule blob for n into out (host), returns its length.
+// Every leaf of numpy's tree for n at depth 6 (64 leaves, one 8192-element chunk): the
+// complete tree block_pw_sum_t64 combines by shuffles.
+static bool leaves_at_depth(int n, int depth) {
+  if (n <= 128) return depth == 0;
+  if (depth == 0) return false;
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return leaves_at_depth(n2, depth - 1) && leaves_at_depth(n - n2, depth - 1);
+}
+bool fmx::pw_tree64(int n) { return n >= 8 && n <= 8192 && leaves_at_depth(n, 6); }
+
 extern "C" int32_t fmx_debug_pw_schedule(int32_t n, int32_t* out, int32_t cap) {
   std::vector<int32_t> s = build_schedule(n);
   int32_t m = (int32_t)std::min<size_t>(s.size(), (size_t)cap);

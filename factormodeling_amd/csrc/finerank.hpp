@@ -301,6 +301,9 @@ __device__ __forceinline__ double fr_inv(double lo, double hi, double kf) {
 template <int K>
 __device__ void fr_build_w0(FrTab& T, uint64_t sample_key, double vmin, double vmax) {
   const int lane = fr_lane();
+  // (a counting-rank sort of the parked samples -- each lane counting the samples below its
+  // own from LDS broadcasts -- measured neutral in the fused pass and 2-7 % slower in the
+  // ranks-only passes, where this sort is on the critical path: the shuffle network stays)
   const uint64_t s = wave_sort64(sample_key == FR_FROM_LDS ? T.spl[lane] : sample_key, lane);
   const uint64_t prev = fr_up(s, 1, lane);
   const int ns = __popcll(__ballot(s != KEY_SENTINEL));

@@ -367,7 +367,7 @@ __device__ __forceinline__ void fr_ic_tail(const FrIc& ic, const FrIcRow& rw, in
 #ifndef FR_FA_LISTS
 #define FR_FA_LISTS 0
 #endif
-template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false, bool ZN = false>
+template <int NT, int EMAX, bool PRES, bool WQ = false, bool IC = false, bool ZN = false, bool T64 = false>
 __global__ void __launch_bounds__(NT, fr_fa_min_waves(NT, EMAX))
 k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, int64_t A, int64_t ld, int method,
              const uint8_t* __restrict__ present, double* __restrict__ Y2, double qlo, double qhi,
@@ -388,6 +388,7 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
   BR_PH_INIT;
   static_assert(!(IC && PRES), "the fused IC ranks dense rows");
   static_assert(!ZN || (WQ && !PRES && !IC), "ZN: dense rank + winsor rows");
+  static_assert(!T64 || (ZN && NT == 512), "T64: the fused pass's 64-leaf moment trees");
   int32_t* zn_sch = reinterpret_cast<int32_t*>(litems);
   double* zn_nodes = reinterpret_cast<double*>(litems + PW_LDS_MAX);
   __shared__ int zn_iscr[ZN ? NW + 2 : 1];
@@ -478,15 +479,20 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     int c1, c2, cnt = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) cnt += (int)wred[w].y;
-    const double s1 = block_pw_sum_w0<NT>([&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; },
-                                          [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c1, table);
+    auto e1 = [&](int i) { const double u = vrow[i]; return u == u ? u : 0.0; };
+    double s1, s2;
+    // T64: the row length's tree is complete over 64 leaves (the launcher checks pw_tree64)
+    if constexpr (T64) s1 = block_pw_sum_t64<NT>(e1, sch, zn_nodes, table);
+    else s1 = block_pw_sum_w0<NT>(e1, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c1, table);
     const double mean = cnt > 0 ? s1 / (double)cnt : qnan();
     BR_PH();
     // (mean - u)^2 for a valid u, 0 for NaN: numpy's (mean - where(nan, 0, u))^2 masked to 0
-    const double s2 = block_pw_sum_w0<NT>([&](int i) {
+    auto e2 = [&](int i) {
       const double u = vrow[i];
       return u == u ? (mean - u) * (mean - u) : 0.0;
-    }, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
+    };
+    if constexpr (T64) s2 = block_pw_sum_t64<NT>(e2, sch, zn_nodes + 8);
+    else s2 = block_pw_sum_w0<NT>(e2, [](int) { return 0; }, sch, zn_nodes, zn_iscr, &c2);
     const double var = cnt > 0 ? s2 / (double)cnt : qnan();
 #endif
     BR_PH();

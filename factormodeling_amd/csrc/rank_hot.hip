@@ -21,6 +21,13 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
   const size_t lds_fr = std::max<size_t>((size_t)A * 8, (size_t)FR_CS_WORDS * 4);
   const int E = br_emax(A, nt_fa);
   const void* k = E < 0 ? nullptr : FMX_EMAX_TABLE(kcrwz_dense)(nt_fa, E);
+  // rows whose numpy moment tree is complete over 64 leaves (4097..8192 assets, e.g. C2's
+  // 5000): the moments combine by shuffles, no serial wave-0 tree walk (block_pw_sum_t64)
+  if (k && nt_fa == 512 && pw_tree64((int)A) && getenv("FMX_ZN_T64") == nullptr) {
+    if (E == 10) k = (const void*)k_cs_rank_fa<512, 10, false, true, false, true, true>;
+    else if (E == 12) k = (const void*)k_cs_rank_fa<512, 12, false, true, false, true, true>;
+    else if (E == 16) k = (const void*)k_cs_rank_fa<512, 16, false, true, false, true, true>;
+  }
   if (rank_impl() == RANK_IMPL_BR || !k || !lds_fits(k, lds_fr)) return FMX_ERR_UNSUPPORTED;
   if (F * D > 0x7fffffffll) { set_error("too many rows for one launch"); return FMX_ERR_UNSUPPORTED; }
   if (F * (d1 - d0) == 0) return FMX_OK;

@@ -167,6 +167,39 @@ __device__ double block_pw_sum_w0(Elem elem, Valid valid, const int32_t* __restr
   return r;
 }
 
+// block_pw_sum for a row whose numpy pairwise tree is COMPLETE over NT/8 = 64 leaves (every
+// leaf at depth 6: pw_tree64(n) on the host, e.g. n = 5000), with no serial combine phase.
+// Thread t forms lane t & 7 of leaf t >> 3 as block_pw_sum_w0 does (the leaf's tail by its
+// lane 0, then broadcast to the 8 lanes); the tree's first three levels pair adjacent leaves,
+// i.e. lanes t ^ 8, t ^ 16, t ^ 32, so they are xor shuffles inside the wave (IEEE + commutes:
+// a node's value does not depend on which child is added first); the wave's subtree sum goes
+// to wsum[wid] and every thread adds the 8 wave sums in the tree's order after one barrier.
+// side(): run by wave 1 before the barrier (as in block_pw_sum_w0).  wsum: 8 doubles per call
+// site (a second call needs its own, or a barrier in between).
+template <int NT, class Elem, class Side = PwNoSide>
+__device__ double block_pw_sum_t64(Elem elem, const int32_t* __restrict__ sched, double* wsum, Side side = Side()) {
+  static_assert(NT == 512, "64 leaves x 8 lanes");
+  PwView s{sched};
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int leaf = tid >> 3, j = tid & 7;
+  const int st = s.lstart(leaf), len = s.llen(leaf), stop = len - (len & 7);
+  double r = elem(st + j);
+  for (int i = 8; i < stop; i += 8) r += elem(st + i + j);
+  r = r + __shfl_xor(r, 1);
+  r = r + __shfl_xor(r, 2);
+  r = r + __shfl_xor(r, 4);
+  if (j == 0)
+    for (int i = stop; i < len; ++i) r += elem(st + i);
+  r = __shfl(r, lane & ~7);                   // the leaf's total (with its tail) to all 8 lanes
+  r = r + __shfl_xor(r, 8);
+  r = r + __shfl_xor(r, 16);
+  r = r + __shfl_xor(r, 32);
+  if (lane == 0) wsum[wid] = r;
+  if (wid == 1) side();
+  __syncthreads();
+  return ((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) + ((wsum[4] + wsum[5]) + (wsum[6] + wsum[7]));
+}
+
 // Exclusive scan of v across the block; *total receives the sum.  scratch: NT/64 ints.
 template <int NT>
 __device__ int block_exscan(int v, int* scratch, int* total) {
@@ -324,6 +357,8 @@ struct PwTable {
 PwTable pw_table(int nmax, fmx_status* err);
 // Host: length in ints of the schedule blob for n.
 int pw_len(int n);
+// Host: numpy's pairwise tree for n is complete over 64 leaves (block_pw_sum_t64 applies).
+bool pw_tree64(int n);
 // Schedules up to this many ints are staged in LDS by the dense-row moment kernels.
 constexpr int PW_LDS_MAX = 1024;
 
