@@ -551,6 +551,8 @@ def main():
     cfg = PL.workload_config(args.workload)
     if os.environ.get("FMX_STEP_STREAMS") == "1":
         cfg.streams = True                      # A/B: the step's independent chains on 3 streams
+    if os.environ.get("FMX_STEP_OVERLAP") == "1":
+        cfg.overlap = True                      # A/B: the rolling set on a side stream
     sp = PL.ShardedPanel(D, A, F, rank, world, dev, seed=0, halo=cfg.halo)
     torch.cuda.synchronize()
 

@@ -62,6 +62,10 @@ class StepConfig:
     # the overlap gains 2.5 % (87.5 vs 89.7 ms/step) while every stage runs 1.4-3x longer
     # under contention (profiles/r02/streams_ab.log)
     streams: bool = False
+    # overlap (round 6, FMX_STEP_OVERLAP=1 for A/B): the rolling set on a side stream for
+    # the whole step, next to the one-pass cross-sectional operators -> Gram -> IC chain on
+    # the current stream (every operator output in its own buffer).  One shard only.
+    overlap: bool = False
 
     @property
     def lookback(self):
@@ -443,7 +447,7 @@ def run_ops(X, cfg: StepConfig, bufs=None, timers=None, be=ENGINE, collect=None,
     owned-date output (tests only); ``side`` (a dict) receives by-products later stages
     reuse (cs_zscore's row stats; "rank2", the doubled ranks of X, written into
     side["rank2_buf"] when it fits).  ``only``: run just the stages it accepts (by name)."""
-    stages = plan_ops(cfg.ops, be, cfg.fuse, zn=zn and not streams and not cfg.streams)
+    stages = plan_ops(cfg.ops, be, cfg.fuse, zn=zn and not cfg.streams)
     offs, need = [], 0
     for _, ops in stages:
         offs.append(need if streams else 0)
@@ -625,6 +629,23 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
     if zn and sp.halo > 0:
         side["zn_dates"] = (sp.halo, sp.X.shape[1])
     early_names = EARLY_STAGES
+    overlap = (cfg.overlap and not cfg.streams and cfg.ops and hasattr(be, "ts_set") and sp.X.is_cuda
+               and sp.world == 1)
+    side_st = None
+    late = os.environ.get("FMX_OVERLAP_LATE") == "1"    # A/B: the rolling set enqueued after the early stages
+
+    def launch_rolling():
+        # the rolling set on its own stream (it reads only X); its outputs get their own
+        # buffers (run_ops with streams: one buffer range per stage)
+        side_st.wait_stream(torch.cuda.current_stream(sp.X.device))
+        sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                          side=side, streams=[side_st], only=lambda n: n.startswith("ts_set:"), zn=zn)
+    if overlap:
+        side_st = getattr(sp, "side_stream", None)
+        if side_st is None:
+            side_st = sp.side_stream = torch.cuda.Stream(sp.X.device)
+        if not late:
+            launch_rolling()
     t0 = _ev(timers)
     halo = sp.exchange_halo_start()
     _rec(timers, "halo", t0)
@@ -635,8 +656,12 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         # dates (from that z-score).  They also process the halo rows, whose outputs are
         # not owned (stale until the exchange lands: the same data every step).
         if cfg.ops:
+            # (overlap: the stream-aware buffer ranges, so no stage shares the rolling set's)
             sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                              own=slice(sp.halo, None), side=side, only=lambda n: n in early_names, zn=zn)
+                              own=slice(sp.halo, None), side=side, streams=[side_st] if overlap else None,
+                              only=lambda n: n in early_names, zn=zn)
+        if overlap and late:
+            launch_rolling()                      # behind the cross-sectional pass, beside the Gram
         if cfg.gram and hasattr(be, "corr_gram"):
             t0 = _ev(timers)
             GN = gram_partials(sp, be, side)
@@ -658,9 +683,14 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         for st in streams:
             st.wait_stream(main)
     if cfg.ops:
-        sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
-                          own=slice(sp.halo, None), side=side, streams=streams,
-                          only=(lambda n: n not in early_names) if early else None, zn=zn)
+        if overlap:                               # the rolling set is already on its stream
+            rest = lambda n: n not in early_names and not n.startswith("ts_set:")  # noqa: E731
+            sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                              own=slice(sp.halo, None), side=side, streams=[side_st], only=rest, zn=zn)
+        else:
+            sp.bufs = run_ops(sp.X, cfg, getattr(sp, "bufs", None), timers=timers, be=be, collect=collect,
+                              own=slice(sp.halo, None), side=side, streams=streams,
+                              only=(lambda n: n not in early_names) if early else None, zn=zn)
     if streams is not None and cfg.gram and hasattr(be, "corr_gram"):
         with torch.cuda.stream(streams[1]):       # right behind cs_zscore's row stats
             t0 = _ev(timers)
@@ -755,6 +785,8 @@ def run_step(sp: ShardedPanel, cfg: StepConfig, timers=None, be=ENGINE, collect=
         top = cfg.top_x if cfg.prune_top_x == "top_x" else cfg.prune_top_x
         kept = be.greedy_prune(C, full_order.cpu().numpy(), cfg.prune_rho, top)
         _rec(timers, "prune", t0)
+    if side_st is not None:                       # join the rolling set
+        torch.cuda.current_stream(sp.X.device).wait_stream(side_st)
     if collect is not None:
         collect.update(daily=full, summ=summ, win=win, C=C, comp=comp)
     return w, kept
