@@ -78,7 +78,7 @@ STAGE_KERNEL = {"ic_daily": ("fmx::k_ic_wave", "fmx::k_ic_daily_br<", "fmx::k_ic
                 "ret:corr": ("fmx::k_ts_corr_fast<", "fmx::k_ts_corr_rl<"), "ret:corr_vol": "fmx::k_ts_corr_feat<", "ret:cvf": "fmx::k_ts_cvf_rl<", "gram": ("fmx::k_gram_zw<", "fmx::k_gram_f64w<", "fmx::k_gram_f64x<"),
                 "cs_zscore_neutralize": "fmx::k_cs_moment_rg<0>",
                 "cs_rank_winsor": "fmx::k_cs_rank_fa<", "cs_rank_winsor_ic": "fmx::k_cs_rank_fa<",
-                "cs_rank_winsor_zn": "fmx::k_cs_rank_fa<512, 10, false, true, false, true>",
+                "cs_rank_winsor_zn": "fmx::k_cs_rank_fa<512, 10, false, true, false, true",
                 "rank_ic": "fmx::k_cs_rank_fa<",
                 "cs_rank": ("fmx::k_cs_rank_br<", "fmx::k_cs_rank_fa<"),
                 "winsor": "fmx::k_cs_quantile_br<0,", "cs:zscore": "fmx::k_cs_moment<0>",

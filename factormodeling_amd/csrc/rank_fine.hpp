@@ -712,10 +712,18 @@ k_cs_rank_fa(const double* __restrict__ X, double* __restrict__ Y, int64_t D, in
     }
     if (RK) __builtin_nontemporal_store((fmx_rank2_t)(key[k] == KEY_SENTINEL ? 0u : (uint32_t)(2 * less + eq + 1)),
                                         RK + row * ld + ia);
-    if (WQ && nv >= 5 && key[k] != KEY_SENTINEL) {
+    if (WQ && nv >= 5) {
+      // the owners of the four order statistics (less <= kk < less + eq) publish their key;
+      // four hits per row, so the divergent stores sit behind a wave-uniform test
+      uint32_t hm = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (less <= kk[j] && kk[j] < less + eq) tval[j] = key[k];   // all writers store the same key
+      for (int j = 0; j < 4; ++j) hm |= ((uint32_t)(kk[j] - less) < (uint32_t)eq ? 1u : 0u) << j;
+      if (key[k] == KEY_SENTINEL) hm = 0;
+      if (__builtin_amdgcn_ballot_w64(hm != 0)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if ((hm >> j) & 1u) tval[j] = key[k];   // all writers store the same key
+      }
     }
   }
   if constexpr (IC) {
