@@ -247,6 +247,30 @@ struct MVSt {
 
 __device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v); }
 
+// ts_decay's weighted window sum sum_k k x_k (k = 1..W oldest -> newest).  The reference is
+// np.dot, i.e. BLAS ddot, whose summation order is the library's (OpenBLAS splits it over
+// SIMD lanes): decay is pinned to |delta| <= 1e-13 sum k|x| / sum k, not bit for bit.  TS_DECAY_SPLIT
+// interleaved fma chains (k mod S) shorten the dependent chain of the register-ring kernels
+// from W to W / S fmas; 1 = one chain.  k_ts_set and k_ts_reg share this function, so the
+// fused and the single-operator outputs stay bit-identical (tests/test_gpu_fused.py).
+#ifndef TS_DECAY_SPLIT
+#define TS_DECAY_SPLIT 4
+#endif
+template <int W>
+__device__ __forceinline__ double decay_dot(const double* ring, int q) {
+  constexpr int S = TS_DECAY_SPLIT < W ? TS_DECAY_SPLIT : W;
+  double a[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) a[j] = 0.0;
+#pragma unroll
+  for (int k = 1; k <= W; ++k) a[(k - 1) % S] = __builtin_fma(ring[(q + k) % W], (double)k, a[(k - 1) % S]);
+  if constexpr (S == 1) return a[0];
+  else if constexpr (S == 2) return a[0] + a[1];
+  else if constexpr (S == 3) return (a[0] + a[1]) + a[2];
+  else return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+
 
 
 // ------------------------------------------------------------------------------------
@@ -352,9 +376,7 @@ __device__ __forceinline__ double ts_step_reg(ColState& c, double v, double* rin
       out = mdiv((double)less + (double)(eq + 1) / 2.0, (double)W, RW);
     } else {
       // oldest element sits in slot q+1 (mod W); weights 1..W oldest->newest
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);   // as BLAS ddot
+      const double acc = decay_dot<W>(ring, q);
       constexpr double DEN = (double)W * (double)(W + 1) / 2.0, RDEN = 1.0 / DEN;
       out = mdiv(acc, DEN, RDEN);
     }
@@ -500,9 +522,7 @@ __device__ __forceinline__ void ts_set_step(SetSt& c, double v, double* ring, in
   if (Yd) {
     double o = qnan();
     if (c.i + 1 >= W && c.nan_w == 0) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 1; k <= W; ++k) acc = __builtin_fma(ring[(q + k) % W], (double)k, acc);
+      const double acc = decay_dot<W>(ring, q);
       constexpr double DEN = (double)W * (double)(W + 1) / 2.0, RDEN = 1.0 / DEN;
       o = mdiv(acc, DEN, RDEN);
     }
