@@ -250,11 +250,13 @@ __device__ __forceinline__ double zsqrt(double v) { return v < 0 ? 0.0 : sqrt(v)
 // ts_decay's weighted window sum sum_k k x_k (k = 1..W oldest -> newest).  The reference is
 // np.dot, i.e. BLAS ddot, whose summation order is the library's (OpenBLAS splits it over
 // SIMD lanes): decay is pinned to |delta| <= 1e-13 sum k|x| / sum k, not bit for bit.  TS_DECAY_SPLIT
-// interleaved fma chains (k mod S) shorten the dependent chain of the register-ring kernels
-// from W to W / S fmas; 1 = one chain.  k_ts_set and k_ts_reg share this function, so the
-// fused and the single-operator outputs stay bit-identical (tests/test_gpu_fused.py).
+// interleaved fma chains (k mod S) would shorten the dependent chain of the register-ring
+// kernels from W to W / S fmas; measured neutral (ts_set 5.14 / 5.18 vs 5.06 / 5.15 ms per
+// 504 dates: the rolling set is bound by its column-walk access pattern), so one chain, the
+// oldest-to-newest order k_ts_win also uses.  k_ts_set and k_ts_reg share this function, so
+// the fused and the single-operator outputs stay bit-identical (tests/test_gpu_fused.py).
 #ifndef TS_DECAY_SPLIT
-#define TS_DECAY_SPLIT 4
+#define TS_DECAY_SPLIT 1
 #endif
 template <int W>
 __device__ __forceinline__ double decay_dot(const double* ring, int q) {
