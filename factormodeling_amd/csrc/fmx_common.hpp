@@ -18,8 +18,9 @@
 // (FR_DIAG_*, GDB_DIAG_*, GW_DIAG).  Each needs -DFMX_DIAG as well, and a translation unit
 // built with FMX_DIAG registers itself at load time, so fmx_build_variant() names the
 // library "diagnostic" and the Python loader refuses it unless FMX_ALLOW_DIAG=1.
-#if !defined(FMX_DIAG) && (defined(FR_DIAG_NOZNSUM) || defined(FR_DIAG_NOSCAN) || defined(FR_DIAG_NOPF) ||      \
-                           defined(FR_DIAG_NOSTORE) || defined(GDB_DIAG_NOSTAGE) || (defined(GW_DIAG) && GW_DIAG != 0))
+#if !defined(FMX_DIAG) &&                                                                           \
+    (defined(FR_DIAG_NOZNSUM) || defined(FR_DIAG_NOSCAN) || defined(FR_DIAG_NOPF) || defined(FR_DIAG_NOSTORE) || \
+     defined(GDB_DIAG_NOSTAGE) || defined(CF_DIAG_RT) || defined(CF_DIAG_NOOLD) || (defined(GW_DIAG) && GW_DIAG != 0))
 #error "diagnostic kernel arms need -DFMX_DIAG (and the library then loads only with FMX_ALLOW_DIAG=1)"
 #endif
 extern "C" void fmx_mark_diag(const char* tu);

@@ -75,7 +75,8 @@ struct MeanSt {
     }
   }
   // result() with the division by the count through mdiv (rt[k] = RN(1 / k), k <= window)
-  __device__ double result_r(int64_t minp, const double* rt) const {
+  template <class RT>
+  __device__ double result_r(int64_t minp, RT rt) const {
     if (n >= minp && n > 0) {
       double r = mdiv(s, (double)n, rt[n]);
       if (same >= n) r = prev;
@@ -130,7 +131,8 @@ struct VarSt {
     }
   }
   // add / remove / var with every division by a count through mdiv (rt[k] = RN(1 / k))
-  __device__ void add_r(double v, const double* rt) {
+  template <class RT>
+  __device__ void add_r(double v, RT rt) {
     if (v != v) return;
     n += 1.0;
     if (v == prev) same += 1; else same = 1;
@@ -142,7 +144,8 @@ struct VarSt {
     mean = mean + mdiv(t, n, rt[(int)n]);
     ssq = ssq + (v - pm) * (v - mean);
   }
-  __device__ void remove_r(double v, const double* rt) {
+  template <class RT>
+  __device__ void remove_r(double v, RT rt) {
     if (v == v) {
       n -= 1.0;
       if (n != 0.0) {
@@ -158,7 +161,8 @@ struct VarSt {
       }
     }
   }
-  __device__ double var_r(int64_t minp, int ddof, const double* rt) const {
+  template <class RT>
+  __device__ double var_r(int64_t minp, int ddof, RT rt) const {
     if (minp < 1) minp = 1;
     if (n >= (double)minp && n > (double)ddof) {
       if (n == 1.0 || (double)same >= n) return 0.0;
@@ -190,7 +194,8 @@ struct MVSt {
     n = neg = same = 0;
     prev = first;
   }
-  __device__ void add_r(double v, const double* rt) {
+  template <class RT>
+  __device__ void add_r(double v, RT rt) {
     if (v == v) {
       n += 1;
       const double y = v - cam, t = s + y;
@@ -206,7 +211,8 @@ struct MVSt {
       ssq = ssq + (v - pm) * (v - mean);
     }
   }
-  __device__ void remove_r(double v, const double* rt) {
+  template <class RT>
+  __device__ void remove_r(double v, RT rt) {
     if (v == v) {
       n -= 1;
       const double y = -v - crm, t = s + y;
@@ -225,7 +231,8 @@ struct MVSt {
       }
     }
   }
-  __device__ double mean_r(int64_t minp, const double* rt) const {   // MeanSt::result_r
+  template <class RT>
+  __device__ double mean_r(int64_t minp, RT rt) const {   // MeanSt::result_r
     if (n >= minp && n > 0) {
       double r = mdiv(s, (double)n, rt[n]);
       if (same >= n) r = prev;
@@ -235,7 +242,8 @@ struct MVSt {
     }
     return qnan();
   }
-  __device__ double var_r(int64_t minp, int ddof, const double* rt) const {   // VarSt::var_r
+  template <class RT>
+  __device__ double var_r(int64_t minp, int ddof, RT rt) const {   // VarSt::var_r
     if (minp < 1) minp = 1;
     if (n >= minp && n > ddof) {
       if (n == 1 || same >= n) return 0.0;
@@ -1076,14 +1084,25 @@ k_ts_corr_fast(const double* __restrict__ X, const double* __restrict__ Ycol, do
 // is written while the corr is in registers: the corr panel is not written and read back,
 // and x / x[d - W] are read once for both.  C (optional, WC) also receives the corr.
 //
+#ifdef CF_DIAG_RT
+struct CfDiagRt {
+  double r;
+  __device__ double operator[](int) const { return r; }
+};
+#endif
 template <int PF, bool WC>
 __global__ void __launch_bounds__(256)
 k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, double* __restrict__ C,
                double* __restrict__ Out, int64_t F, int64_t D, int64_t A, int64_t ld, int64_t y_fstride, int W,
                int64_t nab) {
-  extern __shared__ double rt[];                  // [W + 1]: rt[k] = RN(1 / k)
-  for (int k = threadIdx.x; k <= W; k += 256) rt[k] = 1.0 / (double)k;
+  extern __shared__ double rt_lds[];              // [W + 1]: rt[k] = RN(1 / k)
+  for (int k = threadIdx.x; k <= W; k += 256) rt_lds[k] = 1.0 / (double)k;
   __syncthreads();
+#ifdef CF_DIAG_RT
+  const CfDiagRt rt{1.0 / (double)W};             // diagnostic (wrong results): no table reads
+#else
+  const double* rt = rt_lds;
+#endif
   const int64_t ab = blockIdx.x % nab, fg = blockIdx.x / nab;
   const int64_t f = fg * 4 + (threadIdx.x >> 6), a = ab * 64 + (threadIdx.x & 63);
   if (f >= F || a >= A) return;
@@ -1104,8 +1123,14 @@ k_ts_corr_feat(const double* __restrict__ X, const double* __restrict__ Ycol, do
     const bool in = d < D, old = in && d >= W;
     nx[s] = in ? x[d * ld] : 0.0;
     ny[s] = in ? yc[d * ld] : 0.0;
+#ifdef CF_DIAG_NOOLD
+    nxo[s] = nx[s];                               // diagnostic (wrong results): no leaving-row reads
+    nyo[s] = ny[s];
+    (void)old;
+#else
     nxo[s] = old ? x[(d - W) * ld] : 0.0;
     nyo[s] = old ? yc[(d - W) * ld] : 0.0;
+#endif
   };
 #pragma unroll
   for (int q = 0; q < PF; ++q) fetch(q, q);
