@@ -50,12 +50,15 @@ fmx_status br_cs_rank_winsor_zn(const double* X, double* Yr, double* Yw, double*
 
 // Doubled average ranks only (k_cs_rank_fa with Y = NULL): the rank pass a daily IC over
 // raw factors starts from (fmx_ic_daily_ranked) when no operator output is wanted.
-// Rows of 8193..10240 assets (C5) take the persistent k_cs_rank2_pf (one row per CU, the
-// next row's loads in flight, no spills); FMX_RANK2_PF=0 keeps k_cs_rank_fa for A/B.
+// Rows of 8193..10240 assets (C5): k_cs_rank_fa<1024, 10> at two rows per CU (its 80 KB of
+// keys and a short scan list fit half the LDS; 64 VGPRs) -- 5.52 / 5.54 vs 6.03 / 6.03 ms per
+// 126 dates x 500 factors for the persistent one-row-per-CU k_cs_rank2_pf (128 VGPRs, the
+// next row's loads in flight; round 4's choice), profiles/r06/abM_*.log.  FMX_RANK2_PF=1
+// keeps the persistent kernel for A/B.
 static bool rank2_pf_enabled() {
   static const bool v = [] {
     const char* e = getenv("FMX_RANK2_PF");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }

@@ -94,6 +94,9 @@ constexpr int ICW_WAVES = 4;
 #define ICW_PF 1
 #endif
 constexpr int ICW_EC = 256;   // E entries per (wave, lag); more NaN returns: ICW_PC overflow
+// table word of a block without a first / second entry: both entry fields 0xffff (no doubled
+// rank reaches it: ranks <= 2A <= 32768), so the per-element correction needs no count tests
+constexpr uint64_t ICW_NO_ENTRY = 0xffffffff00000000ull;
 
 #ifndef ICW_MINW
 #define ICW_MINW 6
@@ -103,10 +106,11 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
           int64_t D, int64_t A, int64_t ld, int L0, int L1, int NL, double* __restrict__ out,
           const int32_t* __restrict__ pos, const int32_t* __restrict__ npos, int32_t* __restrict__ ovf) {
   // per wave and lag: the rank-block table T[nbp] (block b = doubled ranks [64b, 64b+64))
-  // and the entries eb[ICW_EC] grouped by block.  T[b] is 64-bit: start | count << 16 of
-  // its E entries in eb, and the block's first two entries (<< 32, << 48; entries are
-  // doubled ranks in [2, 2A], 16 bits): one ds_read_b64 per lag and element instead of the
-  // table word plus two entry reads.  Dynamic LDS: ICW_WAVES * 2 * (2 nbp + ICW_EC) + 2 words.
+  // and the entries eb[ICW_EC] grouped by block.  T[b] is 64-bit: 2 * start | count << 16
+  // of its E entries in eb (2 * start = the correction of every earlier block's entries), and
+  // the block's first two entries (<< 32, << 48; entries are doubled ranks in [2, 2A], 16
+  // bits; 0xffff where absent): one ds_read_b64 per lag and element instead of the table
+  // word plus two entry reads.  Dynamic LDS: ICW_WAVES * 2 * (2 nbp + ICW_EC) + 2 words.
   extern __shared__ uint32_t icw_lds[];
   __shared__ double scr[ICW_WAVES * 32];
   // the wave index as a scalar: the row, its pointers and lags live in SGPRs (saddr loads)
@@ -239,14 +243,14 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     for (int q = 0; q < RMAX; ++q) {
       const int b = lane * R + q;
       st[q] = run;
-      if (q < R && b < nbp) T64[m][b] = (uint64_t)((uint32_t)run | ((uint32_t)cn[q] << 16));
+      if (q < R && b < nbp) T64[m][b] = ICW_NO_ENTRY | (uint64_t)((uint32_t)(2 * run) | ((uint32_t)cn[q] << 16));
       run += cn[q];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int q = 0; q < ICW_EC / 64; ++q)
-      if (er[m][q]) eb[m][((uint32_t)T64[m][er[m][q] >> 6] & 0xffffu) + es[m][q]] = er[m][q];
+      if (er[m][q]) eb[m][(((uint32_t)T64[m][er[m][q] >> 6] & 0xffffu) >> 1) + es[m][q]] = er[m][q];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     // the first two entries of each block into its table word
@@ -254,11 +258,15 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     for (int q = 0; q < RMAX; ++q) {
       const int b = lane * R + q;
       if (q < R && b < nbp && cn[q] > 0) {
-        const uint64_t e0 = eb[m][st[q]], e1 = cn[q] > 1 ? eb[m][st[q] + 1] : 0u;
-        T64[m][b] = (uint64_t)((uint32_t)st[q] | ((uint32_t)cn[q] << 16)) | (e0 << 32) | (e1 << 48);
+        const uint64_t e0 = eb[m][st[q]], e1 = cn[q] > 1 ? eb[m][st[q] + 1] : 0xffffu;
+        T64[m][b] = (uint64_t)((uint32_t)(2 * st[q]) | ((uint32_t)cn[q] << 16)) | (e0 << 32) | (e1 << 48);
       }
     }
   }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)                 // a lag without entries: every block empty
+    if (ne[m] == 0)
+      for (int b = lane; b < nbp; b += 64) T64[m][b] = ICW_NO_ENTRY;
   __builtin_amdgcn_wave_barrier();
   // 2. one pass.  Per lag: pair count (ballots); the first pair's (x, r) is the lag's
   // shift (a, b) and reference (constant inputs: no pair differs from it); sums of x', r',
@@ -294,8 +302,8 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
     }
     if (i0 + 64 * ICW_PF < An) load(i0 + 64 * ICW_PF, ICW_PF - 1);
   };
-  // the pair rank 2k = RK minus the E correction of lag m.  Branch-free for both lags (T is
-  // zeroed, so a lag without E entries reads j0 = j1 = 0): the two lags' table reads issue
+  // the pair rank 2k = RK minus the E correction of lag m.  Branch-free for both lags (a lag
+  // without E entries reads empty blocks): the two lags' table reads issue
   // back to back and share one LDS latency.  The block's first two entries without a loop:
   // with ~1 NaN return per 6 rank blocks nearly every wave has a lane whose block holds
   // one, and a loop there made the whole wave run it (7.75 -> 7.30 ms at C2; a read past the
@@ -303,11 +311,10 @@ k_ic_wave(const double* __restrict__ X, const fmx_rank2_t* __restrict__ RK, cons
   auto pair_rank = [&](int m, uint32_t rk) {
     const uint64_t tb = T64[m][rk >> 6];
     const uint32_t lo = (uint32_t)tb, hi = (uint32_t)(tb >> 32);
-    const uint32_t j0 = lo & 0xffffu, nj = lo >> 16, j1 = j0 + nj;
+    const uint32_t j0 = (lo & 0xffffu) >> 1, nj = lo >> 16, j1 = j0 + nj;
     const uint32_t e0 = hi & 0xffffu, e1 = hi >> 16;
-    int corr = 2 * (int)j0;
-    corr += nj > 0 ? (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) : 0;
-    corr += nj > 1 ? (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0) : 0;
+    // absent entries are 0xffff, above every doubled rank: they count nothing
+    int corr = (int)(lo & 0xffffu) + (e0 < rk ? 1 : 0) + (e0 <= rk ? 1 : 0) + (e1 < rk ? 1 : 0) + (e1 <= rk ? 1 : 0);
     for (uint32_t j = j0 + 2; j < j1; ++j) {   // a third entry or more (rare)
       const uint32_t e = eb[m][j];
       corr += (e < rk ? 1 : 0) + (e <= rk ? 1 : 0);

@@ -313,11 +313,10 @@ def test_cs_rank2_matches_rank_winsor_ranks(dev, A):
     assert np.array_equal(got.cpu().numpy(), ref.cpu().numpy())
 
 
-@pytest.mark.parametrize("A", [8193, 10000, 10240])
-def test_cs_rank2_persistent_rows_vs_rankdata(dev, A):
-    """The persistent ranks-only kernel (k_cs_rank2_pf: one row per CU, the next row's loads
-    in flight) over more rows than the grid holds, with heavy ties, NaN, empty and
-    single-value rows: doubled average ranks = 2 * scipy rankdata(average), 0 for NaN."""
+def _rank2_rows_check(A):
+    """Ranks-only pass over rows of 8193..10240 assets (more rows than the grid holds), with
+    heavy ties, NaN, empty and single-value rows: doubled average ranks = 2 * scipy
+    rankdata(average), 0 for NaN."""
     import torch
     from scipy.stats import rankdata
     import factormodeling_amd.engine as E
@@ -330,7 +329,7 @@ def test_cs_rank2_persistent_rows_vs_rankdata(dev, A):
     X[0, 5] = np.nan                             # empty row
     X[1, 9, 1:] = np.nan                         # single valid value
     X[1, 11] = 2.5                               # one value
-    Xt = torch.as_tensor(X, device=dev)
+    Xt = torch.as_tensor(X, device="cuda")
     got = E.cs_rank2(Xt).cpu().numpy().astype(np.int64)
     for f in range(F):
         for d in range(D):
@@ -340,6 +339,27 @@ def test_cs_rank2_persistent_rows_vs_rankdata(dev, A):
             if ok.any():
                 exp[ok] = np.rint(2 * rankdata(x[ok], method="average")).astype(np.int64)
             assert np.array_equal(got[f, d], exp), (f, d)
+
+
+@pytest.mark.parametrize("A", [8193, 10000, 10240])
+def test_cs_rank2_long_rows_vs_rankdata(dev, A):
+    """The default ranks-only kernel for C5-length rows (k_cs_rank_fa<1024, 10>, two rows per
+    CU where the LDS allows) against scipy."""
+    _rank2_rows_check(A)
+
+
+def test_cs_rank2_persistent_rows_vs_rankdata(dev):
+    """The persistent ranks-only kernel (k_cs_rank2_pf: one row per CU, the next row's loads
+    in flight; FMX_RANK2_PF=1, read once per process: a child process) against scipy."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = ("import sys; sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests'); "
+              "import test_gpu_fused as t\nfor A in (8193, 10000, 10240): t._rank2_rows_check(A)\nprint('OK')")
+    env = dict(os.environ, FMX_RANK2_PF="1")
+    r = subprocess.run([sys.executable, "-c", script, root], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
 def test_ts_set_division_edge_values(dev):
